@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py -- Msamples/s of the relativistic path tracer's hot path on MI355X.
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on): CBbunny.dae at
+1920x1080, 64 spp (adaptive: batch 32, tol 0.05), Schwarzschild black hole (centre (0,1,0),
+r_s 0.1, dtheta 0.1), max_ray_depth 1 -- the reference defaults.  The scene and camera are the
+reference's own, flattened by the oracle harness (tests/golden/scenes/CBbunny.rrts,
+tests/golden/cfg3_bunny_1080p_s64/camera.rrtc); they are HBM-resident before timing.
+
+One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's 32x32
+tiles are split block-cyclically (rrt_partition_tiles); every rank renders its tiles into a
+packed buffer and rank 0 gathers them over RCCL and unpacks them into the frame (the only
+exchange step).  Total work is fixed, so scaling is "strong".
+
+value = actual camera samples in the frame (sum of the per-pixel sampleCountBuffer, i.e.
+adaptive-aware) x steps / max-over-ranks wall time.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
+
+import rrt  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+WORKLOADS = {
+    "cfg3": dict(scene="scenes/CBbunny.rrts", camera="cfg3_bunny_1080p_s64/camera.rrtc", w=1920, h=1080, spp=64,
+                 bh=((0.0, 1.0, 0.0), 0.1, 0.1),
+                 desc="cfg3: CBbunny.dae 1920x1080 64spp, Schwarzschild geodesic (r_s 0.1, dtheta 0.1), depth 1"),
+    "cfg2": dict(scene="scenes/CBspheres_lambertian.rrts", camera="cfg2_spheres_1080p_s64_flat/camera.rrtc", w=1920,
+                 h=1080, spp=64, bh=((0.0, 1.0, 0.0), 0.0, 0.1),
+                 desc="cfg2: CBspheres_lambertian.dae 1920x1080 64spp, flat limit (r_s 0), depth 1"),
+    "cfg1": dict(scene="scenes/CBspheres_lambertian.rrts", camera="cfg1_spheres_480x360_s8/camera.rrtc", w=480,
+                 h=360, spp=8, bh=((0.0, 1.0, 0.0), 0.1, 0.1),
+                 desc="cfg1: CBspheres_lambertian.dae 480x360 8spp, Schwarzschild"),
+}
+TILE = 32
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic bytes
+
+
+def cpu_baseline(wl, threads, row_stride):
+    """The oracle restatement (oracle/restate, bit-exact with the reference) on the host cores,
+    over every `row_stride`-th row of the same frame (a representative bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    s = O.Scene(os.path.join(GOLD, wl["scene"]))
+    cam = O.load_camera(os.path.join(GOLD, wl["camera"]))
+    c, r_s, dt = wl["bh"]
+    p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], bh=(c[0], c[1], c[2], r_s, dt))
+    rows = list(range(row_stride // 2, wl["h"], row_stride))
+    samples = 0
+    t0 = time.perf_counter()
+    for y in rows:
+        _, cnt, _, _ = O.render(s, cam, p, 0, y, wl["w"], 1, threads=threads)
+        samples += int(cnt.sum())
+    dt_s = time.perf_counter() - t0
+    return {"value": samples / dt_s / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"rows {rows[0]}::{row_stride} of the {wl['w']}x{wl['h']} frame ({len(rows)} rows, "
+                      f"{samples} samples, {dt_s:.1f} s); oracle/restate (C, bit-exact with the reference "
+                      f"under the keyed RNG), pthreads over 32-px tiles"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-row-stride", type=int, default=8)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    wl = WORKLOADS[a.workload]
+    W, H = wl["w"], wl["h"]
+
+    r = rrt.Renderer(device=torch.cuda.current_device())
+    scene = rrt.SceneFile(os.path.join(GOLD, wl["scene"]))
+    r.set_scene(scene)
+    r.set_camera(rrt.load_camera(os.path.join(GOLD, wl["camera"])))
+    r.set_black_hole(*wl["bh"])
+    params = rrt.render_params(W, H, ns_aa=wl["spp"])
+
+    tiles = rrt.partition_tiles(W, H, TILE, rank, world)
+    n_max = len(rrt.partition_tiles(W, H, TILE, 0, world))  # rank 0 holds the most tiles
+    tpix = TILE * TILE
+    # packed per-rank result: [n_max * tpix * 3] f32 rgb, then [n_max * tpix] i32 counts
+    packed = torch.zeros(n_max * tpix * 4, dtype=torch.int32, device=dev)
+    p_rgb = packed.data_ptr()
+    p_cnt = packed.data_ptr() + n_max * tpix * 3 * 4
+    stream = torch.cuda.current_stream()
+    s_handle = stream.cuda_stream
+    if rank == 0:
+        frame_rgb = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+        frame_cnt = torch.zeros(H * W, dtype=torch.int32, device=dev)
+        gather_bufs = [torch.zeros_like(packed) for _ in range(world)] if world > 1 else [packed]
+        rank_tiles = [rrt.partition_tiles(W, H, TILE, q, world) for q in range(world)]
+
+    kern_ms = []
+
+    def step(timed):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r.render_tiles_device(params, tiles, TILE, p_rgb, p_cnt, stream=s_handle)
+        e1.record(stream)
+        if world > 1:
+            dist.gather(packed, gather_bufs if rank == 0 else None, dst=0)
+        if rank == 0:
+            for q in range(world):
+                base = gather_bufs[q].data_ptr()
+                r.unpack_tiles_device(rank_tiles[q], TILE, W, H, base, base + n_max * tpix * 3 * 4,
+                                      frame_rgb.data_ptr(), frame_cnt.data_ptr(), stream=s_handle)
+        if timed:
+            kern_ms.append((e0, e1))
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    k_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kern_ms]))
+
+    # algorithmic work of this rank's launch: counting variant, outside the timed region
+    n_loc = len(tiles)
+    ctr = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
+    cparams = rrt.render_params(W, H, ns_aa=wl["spp"], flags=rrt.RRT_RENDER_COUNTERS)
+    tmp = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
+    r.render_tiles_device(cparams, tiles, TILE, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
+                          d_counters=ctr.data_ptr(), stream=s_handle)
+    torch.cuda.synchronize()
+    c4 = ctr.view(-1, 4).to(torch.int64).sum(0).cpu().numpy()
+    cnt_local = tmp[n_loc * tpix * 3:n_loc * tpix * 4].to(torch.int64).sum()
+    pix_local = sum(min(TILE, W - int(x)) * min(TILE, H - int(y)) for x, y in tiles)
+    stats = torch.tensor([float(cnt_local), float(c4[0]), float(c4[1]), float(c4[2]), float(c4[3]), float(pix_local)],
+                         dtype=torch.float64, device=dev)
+    loc_bytes = BYTES_AABB * c4[0] + BYTES_PRIM * c4[2] + BYTES_PIXEL * pix_local
+    if world > 1:
+        dist.all_reduce(stats)
+    samples, bbox, micro, prim, queries, pixels = [float(v) for v in stats.cpu().numpy()]
+
+    if rank == 0:
+        # sanity: the gathered frame holds every pixel's sample count
+        frame_samples = int(frame_cnt.to(torch.int64).sum().item())
+        assert frame_samples == int(samples), (frame_samples, samples)
+        value = samples * a.steps / elapsed / 1e6
+        achieved = loc_bytes / (k_ms * 1e-3) / 1e9
+        out = {
+            "metric": "Msamples/sec (whole node), 1080p 64spp CBbunny + Schwarzschild geodesic"
+            if a.workload == "cfg3" else f"Msamples/sec (whole node), {wl['desc']}",
+            "value": value,
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "reference scene asset (flattened by the oracle harness), keyed RNG seed 0",
+            "config": {"workload": wl["desc"], "frame": [W, H], "spp": wl["spp"], "tile": TILE,
+                       "partition": f"block-cyclic {TILE}x{TILE} tiles over {world} GPU(s), RCCL gather to rank 0"},
+            "samples_per_frame": int(samples),
+            "nominal_msamples_per_s": W * H * wl["spp"] * a.steps / elapsed / 1e6,
+            "kernel_ms_rank0": k_ms,
+            "work_per_sample": {"aabb_tests": bbox / samples, "micro_steps": micro / samples,
+                                "prim_tests": prim / samples, "queries": queries / samples},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "rrt_render_kernel<false,false>",
+                         "algorithmic_bytes_per_launch": float(loc_bytes)},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+            out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+/* rrt.h -- C ABI of the MI355X-native relativistic path-tracer hot path (librrt.so).
+ *
+ * Drop-in boundary for the reference's per-pixel radiance loop.  The reference has no
+ * plugin/FFI API for this path; the seam it replaces is the private C++ call chain
+ *   PathTracer::raytrace_tile  (pathtracer.cpp:549-581, pathtracer.h:212)
+ *     -> PathTracer::raytrace_pixel (part1_code.cpp:125-163)
+ *        -> BVHAccel::intersect (bvh.cpp:103-138) -> BlackHole::next_micro_ray (blackhole.cpp:17-40)
+ *        -> BSDF::sample_f / SceneLight::sample_L (bsdf.cpp, light.cpp)
+ * plus the state its callers install: PathTracer::set_scene (pathtracer.cpp:95-117, which also
+ * builds the BVH, :304-328), set_camera (:119-134), set_frame_size (:136-149) and the `-B`
+ * black-hole override of main.cpp:139-145.  Each entry point below names the reference
+ * interface it replaces.  Plain C types only; no exceptions cross the ABI; every function
+ * returns RRT_OK (0) or a negative RRT_E* code, with a message in rrt_last_error().
+ *
+ * RNG: the reference draws from one shared glibc rand() stream; this library uses the keyed
+ * per-pixel stream of csrc/rrt_rng.h (seed, x, y), which the oracle harness also links into
+ * the reference, so outputs are comparable pixel by pixel.
+ */
+#ifndef RRT_H
+#define RRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RRT_ABI_VERSION 1
+
+enum {
+  RRT_OK = 0,
+  RRT_E_INVALID = -1,     /* bad argument / unsupported scene feature */
+  RRT_E_HIP = -2,         /* HIP runtime error (message has the HIP error string) */
+  RRT_E_CANCELLED = -3,   /* render stopped through the cancel flag (PathTracer::stop) */
+  RRT_E_NO_DEVICE = -4,   /* context created host-only (device < 0) or no GPU */
+  RRT_E_IO = -5           /* file helpers */
+};
+
+typedef struct rrt_ctx rrt_ctx;
+
+/* ---------------------------------------------------------------- context */
+typedef struct {
+  int device;              /* HIP device ordinal; -1 = host-only context (BVH build, tests) */
+  uint32_t reserved[7];
+} rrt_device_cfg;
+
+/* Replaces: PathTracer::PathTracer (pathtracer.cpp:32-85) device-side state. */
+int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg);
+void rrt_destroy(rrt_ctx* ctx);
+const char* rrt_last_error(const rrt_ctx* ctx);
+int rrt_abi_version(void);
+
+/* ---------------------------------------------------------------- scene */
+enum { RRT_OBJ_MESH = 0, RRT_OBJ_SPHERE = 1 };
+/* BSDF kinds and parameter slots: include/rrt_scene_format.h (bsdf.h:74-199) */
+enum { RRT_BSDF_DIFFUSE = 0, RRT_BSDF_EMISSION = 1, RRT_BSDF_MIRROR = 2, RRT_BSDF_GLASS = 3,
+       RRT_BSDF_MICROFACET = 4, RRT_BSDF_REFRACTION = 5 };
+/* Light kinds (light.h): area, point, directional, infinite hemisphere */
+enum { RRT_LIGHT_AREA = 0, RRT_LIGHT_POINT = 1, RRT_LIGHT_DIRECTIONAL = 2, RRT_LIGHT_HEMISPHERE = 3 };
+
+typedef struct {
+  uint32_t kind;              /* RRT_OBJ_* */
+  uint32_t bsdf;              /* index into rrt_scene_desc.bsdfs */
+  uint32_t n_vertices, n_triangles;
+  const double* positions;    /* mesh: [n_vertices][3]   (StaticScene::Mesh::positions) */
+  const double* normals;      /* mesh: [n_vertices][3]   (StaticScene::Mesh::normals) */
+  const uint32_t* indices;    /* mesh: [n_triangles][3], mesh-local (object.cpp:28-33) */
+  double center[3];           /* sphere (SphereObject::o) */
+  double radius;              /* sphere (SphereObject::r) */
+} rrt_object_desc;
+
+typedef struct { uint32_t type; float params[14]; } rrt_bsdf_desc;
+
+typedef struct {
+  uint32_t type, is_delta;
+  float radiance[3];
+  float area;                 /* area light: (float)(|dim_x| * |dim_y|), light.cpp:78 */
+  double v[4][3];             /* area: position, direction, dim_x, dim_y; point: position;
+                                 directional: dirToLight; hemisphere: sampleToWorld columns */
+} rrt_light_desc;
+
+typedef struct {
+  uint32_t n_objects, n_bsdfs, n_lights, reserved;
+  const rrt_object_desc* objects;   /* StaticScene::Scene::objects order = BVH build order */
+  const rrt_bsdf_desc* bsdfs;
+  const rrt_light_desc* lights;     /* StaticScene::Scene::lights order */
+} rrt_scene_desc;
+
+/* Replaces: PathTracer::set_scene + build_accel (pathtracer.cpp:95-117, 304-328;
+ * BVHAccel::construct_bvh bvh.cpp:49-96).  The library copies everything (the caller keeps
+ * ownership), builds the reference BVH on the host and uploads a flattened copy to HBM. */
+int rrt_set_scene(rrt_ctx* ctx, const rrt_scene_desc* scene);
+
+/* ---------------------------------------------------------------- camera / spacetime */
+typedef struct {
+  double hFov, vFov;          /* degrees (Camera::hFov / vFov after configure/set_screen_size) */
+  double nClip, fClip;
+  double pos[3];
+  double c2w[9];              /* row-major c2w(i, j), as Camera::dump_settings writes it */
+  double lensRadius, focalDistance;
+} rrt_camera_desc;
+/* Replaces: PathTracer::set_camera (pathtracer.cpp:119-134). */
+int rrt_set_camera(rrt_ctx* ctx, const rrt_camera_desc* cam);
+
+enum { RRT_METRIC_SCHWARZSCHILD = 0 };
+typedef struct {
+  uint32_t kind;              /* RRT_METRIC_SCHWARZSCHILD (r_s = 0: the reference's flat limit) */
+  uint32_t reserved;
+  double center[3];           /* global_black_hole.o   (blackhole.cpp:5 default (0,1,0)) */
+  double r_s;                 /* global_black_hole.r   (default 0.1) */
+  double delta_theta;         /* global_black_hole.delta_theta (default 0.1) */
+} rrt_spacetime_desc;
+/* Replaces: the `-B x y z r dtheta` override of the global black hole (main.cpp:139-145). */
+int rrt_set_spacetime(rrt_ctx* ctx, const rrt_spacetime_desc* st);
+
+/* ---------------------------------------------------------------- render */
+typedef struct {
+  uint32_t ns_aa;             /* -s   (AppConfig default 1) */
+  uint32_t max_ray_depth;     /* -m   (default 1) */
+  uint32_t ns_area_light;     /* -l   (default 1) */
+  uint32_t samples_per_batch; /* -a n (default 32) */
+  float max_tolerance;        /* -a t (default 0.05f) */
+  uint32_t direct_hemisphere; /* -H */
+  uint64_t seed;              /* keyed RNG seed */
+  uint32_t frame_w, frame_h;  /* sampleBuffer.w / h (set_frame_size) */
+  uint32_t flags;             /* RRT_RENDER_* */
+  uint32_t reserved;
+} rrt_render_params;
+enum {
+  RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
+  RRT_RENDER_DRAWS = 1u << 1     /* also produce per-pixel RNG draw counts */
+};
+void rrt_render_params_default(rrt_render_params* p);
+
+/* Replaces: PathTracer::raytrace_tile / raytrace_cell over the region [x0,x0+w) x [y0,y0+h)
+ * of the frame (y = 0 at the bottom, sampleBuffer rows).  Host buffers, row-major over the
+ * region: rgb_out [h][w][3] (sampleBuffer Spectrum), count_out [h][w]
+ * (sampleCountBuffer, part1_code.cpp:161).  draws_out [h][w] and counters_out [h][w][4]
+ * (AABB tests, micro steps, primitive tests, BVH queries) are optional (NULL).
+ * cancel: polled between launches (continueRaytracing, pathtracer.cpp:566); may be NULL. */
+int rrt_render(rrt_ctx* ctx, const rrt_render_params* p, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+               float* rgb_out, int32_t* count_out, uint32_t* draws_out, uint32_t* counters_out,
+               const volatile int* cancel);
+
+/* Device-resident variant for multi-GPU / benchmarking.  Renders the listed square tiles
+ * (tile t covers x in [tiles[2t], +tile_size), y in [tiles[2t+1], +tile_size), clipped to
+ * the frame) into PACKED device buffers: pixel (i, j) of list entry t goes to
+ * rgb[(t * tile_size * tile_size + j * tile_size + i) * 3], count[...] likewise.  Asynchronous
+ * on `stream` (a hipStream_t, NULL = default stream); no host synchronisation.
+ * tiles is a host array of 2*n_tiles uint32. */
+int rrt_render_tiles_device(rrt_ctx* ctx, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles,
+                            uint32_t tile_size, float* d_rgb, int32_t* d_count, uint32_t* d_counters,
+                            void* stream);
+/* Unpack packed tiles (as written above) into frame-layout device buffers [frame_h][frame_w]. */
+int rrt_unpack_tiles_device(rrt_ctx* ctx, const uint32_t* tiles, uint32_t n_tiles, uint32_t tile_size,
+                            uint32_t frame_w, uint32_t frame_h, const float* d_rgb_packed,
+                            const int32_t* d_count_packed, float* d_rgb, int32_t* d_count, void* stream);
+/* Gamma tonemap to RGBA8, HDRImageBuffer::toColor + ImageBuffer::update_pixel
+ * (image.h:53-62, 183-198), frame layout on the device. */
+int rrt_tonemap_device(rrt_ctx* ctx, uint32_t n_pixels, const float* d_rgb, uint32_t* d_rgba, void* stream);
+
+/* Block-cyclic tile partition of a frame over `world` ranks (serpentine 32x32 tile order,
+ * multi-GPU split of SURVEY 8(e)).  Writes up to max_tiles (x, y) pairs for `rank` into
+ * tiles_out and returns the number of tiles (or a negative error). */
+int rrt_partition_tiles(uint32_t frame_w, uint32_t frame_h, uint32_t tile_size, uint32_t rank, uint32_t world,
+                        uint32_t* tiles_out, uint32_t max_tiles);
+
+/* ---------------------------------------------------------------- introspection */
+typedef struct {
+  uint32_t n_prims, n_nodes, n_leaf_refs, max_depth;
+  uint64_t device_bytes;      /* HBM held by the scene */
+  float last_kernel_ms;       /* HIP-event time of the last render launch */
+  uint32_t grid_blocks, block_threads;
+} rrt_stats;
+int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
+/* Host copy of the flattened BVH: boxes [n][6] (min, max), nodes [n][4] (first, count, left,
+ * right; count 0 = inner node), prims [n_leaf_refs] (build-order primitive ids) -- the layout
+ * of the oracle's reference-BVH dump.  Any pointer may be NULL to query sizes via stats. */
+int rrt_get_bvh(const rrt_ctx* ctx, double* boxes, int32_t* nodes, uint32_t* prims);
+
+/* ---------------------------------------------------------------- file helpers (.rrts/.rrtc) */
+typedef struct rrt_scene_file rrt_scene_file;
+int rrt_scene_file_load(const char* path, rrt_scene_file** out);
+const rrt_scene_desc* rrt_scene_file_desc(const rrt_scene_file* f);
+void rrt_scene_file_free(rrt_scene_file* f);
+int rrt_camera_file_load(const char* path, rrt_camera_desc* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RRT_H */

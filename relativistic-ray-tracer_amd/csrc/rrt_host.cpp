@@ -1,0 +1,673 @@
+// rrt_host.cpp -- C ABI (include/rrt.h): scene flattening, the reference BVH build, camera and
+// spacetime set-up, HBM residency and kernel launches.
+//
+// Host-side work the reference does once per frame (PathTracer::set_scene -> build_accel,
+// pathtracer.cpp:95-117, 304-328; BVHAccel::construct_bvh, bvh.cpp:49-96) is reproduced in C++
+// here with the reference's arithmetic (std::min/max, centroid = (min + max) * (1.0 / 2)), so the
+// BVH is node-for-node the reference's; it is then laid out for the GPU (rrt_internal.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rrt.h"
+#include "../../include/rrt_scene_format.h"
+#include "rrt_internal.h"
+
+hipError_t rrt_launch_render(const KParams& kp, int deep, int count, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
+                             const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
+hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
+                              hipStream_t stream);
+
+namespace {
+
+constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
+
+struct V3 { double x, y, z; };
+inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
+inline V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+
+struct Box {
+  V3 mx, mn, ext;
+  static Box empty() {
+    Box b; b.mx = mk(-INFINITY, -INFINITY, -INFINITY); b.mn = mk(INFINITY, INFINITY, INFINITY); b.ext = sub(b.mx, b.mn);
+    return b;
+  }
+  static Box point(V3 p) { Box b; b.mn = p; b.mx = p; b.ext = sub(b.mx, b.mn); return b; }
+  void expand(V3 p) {
+    mn.x = smin(mn.x, p.x); mn.y = smin(mn.y, p.y); mn.z = smin(mn.z, p.z);
+    mx.x = smax(mx.x, p.x); mx.y = smax(mx.y, p.y); mx.z = smax(mx.z, p.z);
+    ext = sub(mx, mn);
+  }
+  void expand(const Box& o) {
+    mn.x = smin(mn.x, o.mn.x); mn.y = smin(mn.y, o.mn.y); mn.z = smin(mn.z, o.mn.z);
+    mx.x = smax(mx.x, o.mx.x); mx.y = smax(mx.y, o.mx.y); mx.z = smax(mx.z, o.mx.z);
+    ext = sub(mx, mn);
+  }
+  V3 centroid() const {  // (min + max) / 2 with Vector3D::operator/ (rc = 1.0 / c)
+    const double rc = 1.0 / 2;
+    V3 s = add(mn, mx);
+    return mk(rc * s.x, rc * s.y, rc * s.z);
+  }
+};
+
+struct Prim {  // build-order primitive
+  uint32_t kind, bsdf;
+  uint32_t v[3];       // triangle: global vertex indices
+  V3 c; double r, r2;  // sphere
+};
+
+struct BNode { Box bb; int32_t first, count, left, right, skip; };
+
+}  // namespace
+
+struct rrt_ctx {
+  int device = -1;
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int n_cu = 256;
+  // host scene
+  std::vector<V3> pos, nrm;
+  std::vector<Prim> prims;
+  std::vector<BNode> nodes;
+  std::vector<uint32_t> leaf;
+  uint32_t max_depth = 0;
+  std::vector<DBsdf> bsdfs;
+  std::vector<DLight> lights;
+  bool has_scene = false, has_camera = false;
+  DCamera cam{};
+  DHole hole{};
+  // device scene
+  DNode* d_nodes = nullptr;
+  DPrimGeo* d_geo = nullptr;
+  DPrimNrm* d_nrm = nullptr;
+  DPrimMeta* d_meta = nullptr;
+  DBsdf* d_bsdfs = nullptr;
+  DLight* d_lights = nullptr;
+  uint64_t device_bytes = 0;
+  // per-launch workspace
+  uint32_t* d_counter = nullptr;
+  uint32_t* d_tiles = nullptr;
+  size_t tiles_cap = 0;
+  float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
+  size_t px_cap = 0;
+  float last_ms = 0.f;
+  bool timed = false;
+  uint32_t last_grid = 0;
+};
+
+static int fail(rrt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(c, x)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(c, RRT_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static void free_scene_dev(rrt_ctx* c) {
+  if (c->device < 0) return;
+  hipFree(c->d_nodes); hipFree(c->d_geo); hipFree(c->d_nrm); hipFree(c->d_meta); hipFree(c->d_bsdfs);
+  hipFree(c->d_lights);
+  c->d_nodes = nullptr; c->d_geo = nullptr; c->d_nrm = nullptr; c->d_meta = nullptr; c->d_bsdfs = nullptr;
+  c->d_lights = nullptr;
+  c->device_bytes = 0;
+}
+
+extern "C" {
+
+int rrt_abi_version(void) { return RRT_ABI_VERSION; }
+
+int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
+  if (!out) return RRT_E_INVALID;
+  std::unique_ptr<rrt_ctx> c(new rrt_ctx());
+  c->device = cfg ? cfg->device : 0;
+  // default spacetime: global_black_hole (blackhole.cpp:5)
+  rrt_spacetime_desc st{};
+  st.kind = RRT_METRIC_SCHWARZSCHILD; st.center[1] = 1.0; st.r_s = 0.1; st.delta_theta = 0.1;
+  if (c->device >= 0) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= c->device) { *out = nullptr; return RRT_E_NO_DEVICE; }
+    if (hipSetDevice(c->device) != hipSuccess) { *out = nullptr; return RRT_E_HIP; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_counter, 64) != hipSuccess) {
+      *out = nullptr;
+      return RRT_E_HIP;
+    }
+  }
+  rrt_set_spacetime(c.get(), &st);
+  *out = c.release();
+  return RRT_OK;
+}
+
+void rrt_destroy(rrt_ctx* c) {
+  if (!c) return;
+  if (c->device >= 0) {
+    hipSetDevice(c->device);
+    free_scene_dev(c);
+    hipFree(c->d_counter); hipFree(c->d_tiles); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
+    hipFree(c->d_ctr);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char* rrt_last_error(const rrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void rrt_render_params_default(rrt_render_params* p) {  // AppConfig defaults, application.h:45-62
+  std::memset(p, 0, sizeof(*p));
+  p->ns_aa = 1; p->max_ray_depth = 1; p->ns_area_light = 1; p->samples_per_batch = 32;
+  p->max_tolerance = 0.05f; p->direct_hemisphere = 0; p->seed = 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------- BVH build
+static Box prim_box(const rrt_ctx* c, const Prim& p) {
+  if (p.kind == RRT_OBJ_MESH) {  // Triangle::get_bbox (triangle.cpp:11-19)
+    Box b = Box::point(c->pos[p.v[0]]);
+    b.expand(c->pos[p.v[1]]);
+    b.expand(c->pos[p.v[2]]);
+    return b;
+  }
+  Box b;  // Sphere::get_bbox (sphere.h:30-32)
+  b.mn = sub(p.c, mk(p.r, p.r, p.r)); b.mx = add(p.c, mk(p.r, p.r, p.r)); b.ext = sub(b.mx, b.mn);
+  return b;
+}
+
+// BVHAccel::construct_bvh (bvh.cpp:49-96): leaf if <= max_leaf_size (4); split at the bbox
+// centroid of the strictly longest axis (ties -> z); centroid < c goes left; if one side is
+// empty, split the list in halves.  Emitted in left-first pre-order.
+static int build(rrt_ctx* c, const std::vector<uint32_t>& ids, uint32_t depth) {
+  Box bb = Box::empty();
+  for (uint32_t id : ids) bb.expand(prim_box(c, c->prims[id]));
+  int me = (int)c->nodes.size();
+  c->nodes.push_back(BNode{bb, 0, 0, -1, -1, -1});
+  c->max_depth = std::max(c->max_depth, depth);
+  if (ids.size() <= 4) {
+    c->nodes[me].first = (int32_t)c->leaf.size();
+    c->nodes[me].count = (int32_t)ids.size();
+    c->leaf.insert(c->leaf.end(), ids.begin(), ids.end());
+    return me;
+  }
+  std::vector<uint32_t> L, R;
+  int axis = (bb.ext.x > bb.ext.y && bb.ext.x > bb.ext.z) ? 0 : (bb.ext.y > bb.ext.x && bb.ext.y > bb.ext.z) ? 1 : 2;
+  V3 cc = bb.centroid();
+  double cv = axis == 0 ? cc.x : axis == 1 ? cc.y : cc.z;
+  for (uint32_t id : ids) {
+    V3 pc = prim_box(c, c->prims[id]).centroid();
+    double v = axis == 0 ? pc.x : axis == 1 ? pc.y : pc.z;
+    (v < cv ? L : R).push_back(id);
+  }
+  if (L.empty() || R.empty()) {
+    L.assign(ids.begin(), ids.begin() + ids.size() / 2);
+    R.assign(ids.begin() + ids.size() / 2, ids.end());
+  }
+  int l = build(c, L, depth + 1);
+  int r = build(c, R, depth + 1);
+  c->nodes[me].left = l;
+  c->nodes[me].right = r;
+  return me;
+}
+
+static int upload(rrt_ctx* c, void** dst, const void* src, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  HIPCHK(c, hipMalloc(dst, bytes));
+  if (src) HIPCHK(c, hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  c->device_bytes += bytes;
+  return RRT_OK;
+}
+
+extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
+  if (!c || !s) return fail(c, RRT_E_INVALID, "null argument");
+  if (s->n_bsdfs > RRT_MAX_BSDFS) return fail(c, RRT_E_INVALID, "too many BSDFs (max 64)");
+  if (s->n_lights > RRT_MAX_LIGHTS) return fail(c, RRT_E_INVALID, "too many lights (max 16)");
+  if (s->n_objects && !s->objects) return fail(c, RRT_E_INVALID, "objects missing");
+  if (s->n_bsdfs && !s->bsdfs) return fail(c, RRT_E_INVALID, "bsdfs missing");
+  if (s->n_lights && !s->lights) return fail(c, RRT_E_INVALID, "lights missing");
+  c->pos.clear(); c->nrm.clear(); c->prims.clear(); c->nodes.clear(); c->leaf.clear(); c->max_depth = 0;
+  c->bsdfs.assign(s->n_bsdfs, DBsdf{});
+  for (uint32_t i = 0; i < s->n_bsdfs; ++i) {
+    if (s->bsdfs[i].type > RRT_BSDF_REFRACTION) return fail(c, RRT_E_INVALID, "unknown BSDF type");
+    c->bsdfs[i].type = s->bsdfs[i].type;
+    std::memcpy(c->bsdfs[i].p, s->bsdfs[i].params, sizeof(float) * 14);
+  }
+  c->lights.assign(s->n_lights, DLight{});
+  for (uint32_t i = 0; i < s->n_lights; ++i) {
+    const rrt_light_desc& L = s->lights[i];
+    if (L.type > RRT_LIGHT_HEMISPHERE)
+      return fail(c, RRT_E_INVALID, "unsupported light type (spot/sphere/mesh lights are stubs in the reference; "
+                                    "environment maps are not implemented yet)");
+    DLight& d = c->lights[i];
+    d.type = L.type; d.is_delta = L.is_delta;
+    std::memcpy(d.rad, L.radiance, sizeof(d.rad)); d.area = L.area;
+    std::memcpy(d.v, L.v, sizeof(d.v));
+  }
+  for (uint32_t o = 0; o < s->n_objects; ++o) {
+    const rrt_object_desc& ob = s->objects[o];
+    if (ob.bsdf >= s->n_bsdfs) return fail(c, RRT_E_INVALID, "object bsdf index out of range");
+    if (ob.kind == RRT_OBJ_MESH) {
+      if ((ob.n_vertices && (!ob.positions || !ob.normals)) || (ob.n_triangles && !ob.indices))
+        return fail(c, RRT_E_INVALID, "mesh arrays missing");
+      uint32_t base = (uint32_t)c->pos.size();
+      for (uint32_t v = 0; v < ob.n_vertices; ++v) {
+        c->pos.push_back(mk(ob.positions[3 * v], ob.positions[3 * v + 1], ob.positions[3 * v + 2]));
+        c->nrm.push_back(mk(ob.normals[3 * v], ob.normals[3 * v + 1], ob.normals[3 * v + 2]));
+      }
+      for (uint32_t t = 0; t < ob.n_triangles; ++t) {
+        Prim p{};
+        p.kind = RRT_OBJ_MESH; p.bsdf = ob.bsdf;
+        for (int k = 0; k < 3; ++k) {
+          uint32_t id = ob.indices[3 * t + k];
+          if (id >= ob.n_vertices) return fail(c, RRT_E_INVALID, "triangle index out of range");
+          p.v[k] = base + id;
+        }
+        c->prims.push_back(p);
+      }
+    } else if (ob.kind == RRT_OBJ_SPHERE) {
+      Prim p{};
+      p.kind = RRT_OBJ_SPHERE; p.bsdf = ob.bsdf;
+      p.c = mk(ob.center[0], ob.center[1], ob.center[2]); p.r = ob.radius; p.r2 = ob.radius * ob.radius;
+      c->prims.push_back(p);
+    } else {
+      return fail(c, RRT_E_INVALID, "unknown object kind");
+    }
+  }
+  if (c->prims.empty()) return fail(c, RRT_E_INVALID, "scene has no primitives");
+  std::vector<uint32_t> ids(c->prims.size());
+  for (size_t i = 0; i < ids.size(); ++i) ids[i] = (uint32_t)i;
+  build(c, ids, 0);
+  // skip pointers: pre-order successor of each subtree
+  c->nodes[0].skip = -1;
+  for (size_t i = 0; i < c->nodes.size(); ++i) {
+    BNode& n = c->nodes[i];
+    if (n.count == 0) {
+      c->nodes[n.left].skip = n.right;
+      c->nodes[n.right].skip = n.skip;
+    }
+  }
+  // device layout
+  std::vector<DNode> dn(c->nodes.size());
+  for (size_t i = 0; i < c->nodes.size(); ++i) {
+    const BNode& n = c->nodes[i];
+    DNode& d = dn[i];
+    d.mn[0] = n.bb.mn.x; d.mn[1] = n.bb.mn.y; d.mn[2] = n.bb.mn.z;
+    d.mx[0] = n.bb.mx.x; d.mx[1] = n.bb.mx.y; d.mx[2] = n.bb.mx.z;
+    d.skip = n.skip; d.first = n.first; d.count = n.count; d.pad = 0;
+  }
+  std::vector<DPrimGeo> geo(c->leaf.size());
+  std::vector<DPrimNrm> nrm(c->leaf.size());
+  std::vector<DPrimMeta> meta(c->leaf.size());
+  for (size_t k = 0; k < c->leaf.size(); ++k) {
+    const Prim& p = c->prims[c->leaf[k]];
+    std::memset(&geo[k], 0, sizeof(DPrimGeo));
+    std::memset(&nrm[k], 0, sizeof(DPrimNrm));
+    if (p.kind == RRT_OBJ_MESH) {
+      V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
+      double g[9] = {p0.x, p0.y, p0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z};
+      std::memcpy(geo[k].v, g, sizeof(g));
+      for (int j = 0; j < 3; ++j) {
+        V3 n = c->nrm[p.v[j]];
+        nrm[k].n[3 * j] = n.x; nrm[k].n[3 * j + 1] = n.y; nrm[k].n[3 * j + 2] = n.z;
+      }
+      meta[k] = (p.bsdf << 8);
+    } else {
+      double g[9] = {p.c.x, p.c.y, p.c.z, p.r2, p.r, 0, 0, 0, 0};
+      std::memcpy(geo[k].v, g, sizeof(g));
+      meta[k] = (p.bsdf << 8) | 1u;
+    }
+  }
+  c->has_scene = true;
+  if (c->device < 0) return RRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  free_scene_dev(c);
+  int rc;
+  if ((rc = upload(c, (void**)&c->d_nodes, dn.data(), dn.size() * sizeof(DNode)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_geo, geo.data(), geo.size() * sizeof(DPrimGeo)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_nrm, nrm.data(), nrm.size() * sizeof(DPrimNrm)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_meta, meta.data(), meta.size() * sizeof(DPrimMeta)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_bsdfs, c->bsdfs.data(), c->bsdfs.size() * sizeof(DBsdf)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_lights, c->lights.data(), c->lights.size() * sizeof(DLight)))) return rc;
+  return RRT_OK;
+}
+
+extern "C" int rrt_set_camera(rrt_ctx* c, const rrt_camera_desc* cam) {
+  if (!c || !cam) return fail(c, RRT_E_INVALID, "null argument");
+  DCamera& d = c->cam;
+  for (int i = 0; i < 3; ++i) {
+    d.pos[i] = cam->pos[i];
+    d.c2w0[i] = cam->c2w[3 * i + 0];  // column 0 = (c2w(0,0), c2w(1,0), c2w(2,0))
+    d.c2w1[i] = cam->c2w[3 * i + 1];
+    d.c2w2[i] = cam->c2w[3 * i + 2];
+  }
+  // Camera::generate_ray (part1_code.cpp:183): bl = (-tan(radians(hFov)/2), -tan(radians(vFov)/2)),
+  // radians(deg) = deg * (PI / 180) (misc.h:49-52); host libm == the reference's values.
+  d.blx = -std::tan(cam->hFov * (kPI / 180) / 2);
+  d.bly = -std::tan(cam->vFov * (kPI / 180) / 2);
+  c->has_camera = true;
+  return RRT_OK;
+}
+
+extern "C" int rrt_set_spacetime(rrt_ctx* c, const rrt_spacetime_desc* st) {
+  if (!c || !st) return fail(c, RRT_E_INVALID, "null argument");
+  if (st->kind != RRT_METRIC_SCHWARZSCHILD) return fail(c, RRT_E_INVALID, "only the Schwarzschild metric is implemented");
+  if (!(st->delta_theta > 0)) return fail(c, RRT_E_INVALID, "delta_theta must be > 0");
+  DHole& h = c->hole;
+  for (int i = 0; i < 3; ++i) h.c[i] = st->center[i];
+  h.r = st->r_s; h.r2 = st->r_s * st->r_s; h.dt = st->delta_theta;
+  h.cos_dt = std::cos(h.dt); h.sin_dt = std::sin(h.dt);  // blackhole.cpp:36-37, host libm
+  int j = 0;
+  while (j * h.dt < 2 * M_PI) ++j;  // bvh.cpp:105
+  h.steps = j;
+  return RRT_OK;
+}
+
+extern "C" int rrt_partition_tiles(uint32_t fw, uint32_t fh, uint32_t ts, uint32_t rank, uint32_t world,
+                                   uint32_t* out, uint32_t max_tiles) {
+  if (ts == 0 || world == 0 || rank >= world) return RRT_E_INVALID;
+  uint32_t tw = (fw + ts - 1) / ts, th = (fh + ts - 1) / ts, n = 0, k = 0;
+  for (uint32_t ty = 0; ty < th; ++ty) {
+    for (uint32_t i = 0; i < tw; ++i, ++k) {
+      uint32_t tx = (ty & 1) ? (tw - 1 - i) : i;  // serpentine
+      if (k % world != rank) continue;
+      if (out && n < max_tiles) { out[2 * n] = tx * ts; out[2 * n + 1] = ty * ts; }
+      ++n;
+    }
+  }
+  return (int)n;
+}
+
+static int ensure(rrt_ctx* c, void** p, size_t& cap, size_t need, size_t elem) {
+  (void)cap;
+  if (need == 0) need = 1;
+  hipFree(*p);
+  *p = nullptr;
+  HIPCHK(c, hipMalloc(p, need * elem));
+  return RRT_OK;
+}
+
+static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles, uint32_t ts,
+                  uint32_t cx0, uint32_t cy0, uint32_t cx1, uint32_t cy1, float* d_rgb, int32_t* d_cnt,
+                  uint32_t* d_draws, uint32_t* d_ctr, hipStream_t stream) {
+  if (!c->has_scene) return fail(c, RRT_E_INVALID, "no scene (rrt_set_scene)");
+  if (!c->has_camera) return fail(c, RRT_E_INVALID, "no camera (rrt_set_camera)");
+  if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "host-only context cannot render");
+  if (p->frame_w == 0 || p->frame_h == 0) return fail(c, RRT_E_INVALID, "frame size is zero");
+  if (p->samples_per_batch == 0) return fail(c, RRT_E_INVALID, "samples_per_batch must be > 0");
+  if (p->max_ray_depth > RRT_MAX_DEPTH) return fail(c, RRT_E_INVALID, "max_ray_depth > 16 not supported");
+  if (ts == 0 || ts % 8 != 0) return fail(c, RRT_E_INVALID, "tile_size must be a positive multiple of 8");
+  if (n_tiles == 0) return RRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->tiles_cap < n_tiles) {
+    hipFree(c->d_tiles); c->d_tiles = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_tiles, sizeof(uint32_t) * 2 * n_tiles));
+    c->tiles_cap = n_tiles;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_tiles, tiles, sizeof(uint32_t) * 2 * n_tiles, hipMemcpyHostToDevice, stream));
+  HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 64, stream));
+  KParams kp{};
+  kp.nodes = c->d_nodes; kp.geo = c->d_geo; kp.nrm = c->d_nrm; kp.meta = c->d_meta;
+  kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size();
+  kp.cam = c->cam; kp.hole = c->hole;
+  kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
+  kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
+  kp.direct_hemisphere = p->direct_hemisphere; kp.seed = p->seed;
+  kp.frame_w = (double)p->frame_w; kp.frame_h = (double)p->frame_h;
+  kp.frame_wi = p->frame_w; kp.frame_hi = p->frame_h;
+  kp.tiles = c->d_tiles; kp.n_tiles = n_tiles; kp.tile_size = ts;
+  kp.blocks_per_tile_side = ts / 8;
+  kp.n_blocks = n_tiles * (ts / 8) * (ts / 8);
+  kp.block_counter = c->d_counter;
+  kp.clip_x0 = cx0; kp.clip_y0 = cy0; kp.clip_x1 = cx1; kp.clip_y1 = cy1;
+  kp.rgb = d_rgb; kp.count = d_cnt; kp.draws = d_draws; kp.counters = d_ctr;
+  // persistent grid: 4 waves per block, at most 4 blocks per CU resident, never more blocks
+  // than there are 8x8 pixel blocks to pull
+  uint32_t want = (kp.n_blocks + 3) / 4;
+  uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 4u);
+  if (grid == 0) grid = 1;
+  c->last_grid = grid;
+  const int deep = p->max_ray_depth >= 2 ? 1 : 0;
+  const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
+  HIPCHK(c, hipEventRecord(c->ev0, stream));
+  HIPCHK(c, rrt_launch_render(kp, deep, count, grid, stream));
+  HIPCHK(c, hipEventRecord(c->ev1, stream));
+  c->timed = true;
+  return RRT_OK;
+}
+
+extern "C" int rrt_render_tiles_device(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
+                                       uint32_t n_tiles, uint32_t ts, float* d_rgb, int32_t* d_count,
+                                       uint32_t* d_counters, void* stream) {
+  if (!c || !p || (n_tiles && (!tiles || !d_rgb || !d_count))) return fail(c, RRT_E_INVALID, "null argument");
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)0;
+  return launch(c, p, tiles, n_tiles, ts, 0, 0, p->frame_w, p->frame_h, d_rgb, d_count, nullptr, d_counters, s);
+}
+
+extern "C" int rrt_unpack_tiles_device(rrt_ctx* c, const uint32_t* tiles, uint32_t n_tiles, uint32_t ts,
+                                       uint32_t fw, uint32_t fh, const float* rgb_p, const int32_t* cnt_p,
+                                       float* rgb, int32_t* cnt, void* stream) {
+  if (!c || c->device < 0) return fail(c, RRT_E_NO_DEVICE, "no device");
+  if (n_tiles == 0) return RRT_OK;
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)0;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->tiles_cap < n_tiles) {
+    hipFree(c->d_tiles); c->d_tiles = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_tiles, sizeof(uint32_t) * 2 * n_tiles));
+    c->tiles_cap = n_tiles;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_tiles, tiles, sizeof(uint32_t) * 2 * n_tiles, hipMemcpyHostToDevice, s));
+  HIPCHK(c, rrt_launch_unpack(c->d_tiles, n_tiles, ts, fw, fh, rgb_p, cnt_p, rgb, cnt, s));
+  return RRT_OK;
+}
+
+extern "C" int rrt_tonemap_device(rrt_ctx* c, uint32_t n, const float* rgb, uint32_t* rgba, void* stream) {
+  if (!c || c->device < 0) return fail(c, RRT_E_NO_DEVICE, "no device");
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)0;
+  // HDRImageBuffer::toColor: gamma 2.2f, level 1.0f, exposure = sqrt(pow(2, level))
+  const float inv_gamma = 1.0f / 2.2f;
+  const float exposure = (float)std::sqrt(std::pow(2, 1.0f));
+  HIPCHK(c, rrt_launch_tonemap(n, rgb, rgba, exposure, inv_gamma, s));
+  return RRT_OK;
+}
+
+extern "C" int rrt_render(rrt_ctx* c, const rrt_render_params* p, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                          float* rgb_out, int32_t* count_out, uint32_t* draws_out, uint32_t* counters_out,
+                          const volatile int* cancel) {
+  if (!c || !p || !rgb_out || !count_out) return fail(c, RRT_E_INVALID, "null argument");
+  if (w == 0 || h == 0) return RRT_OK;
+  if ((uint64_t)x0 + w > p->frame_w || (uint64_t)y0 + h > p->frame_h) return fail(c, RRT_E_INVALID, "region outside frame");
+  if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "host-only context cannot render");
+  if (cancel && *cancel) return fail(c, RRT_E_CANCELLED, "cancelled");
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t ts = 32;
+  std::vector<uint32_t> tiles;
+  for (uint32_t ty = y0; ty < y0 + h; ty += ts)
+    for (uint32_t tx = x0; tx < x0 + w; tx += ts) { tiles.push_back(tx); tiles.push_back(ty); }
+  const uint32_t nt = (uint32_t)(tiles.size() / 2);
+  const size_t npx = (size_t)nt * ts * ts;
+  if (c->px_cap < npx) {
+    size_t dummy = 0;
+    int rc;
+    if ((rc = ensure(c, (void**)&c->d_rgb, dummy, npx, 3 * sizeof(float)))) return rc;
+    if ((rc = ensure(c, (void**)&c->d_cnt, dummy, npx, sizeof(int32_t)))) return rc;
+    if ((rc = ensure(c, (void**)&c->d_draws, dummy, npx, sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, (void**)&c->d_ctr, dummy, npx, 4 * sizeof(uint32_t)))) return rc;
+    c->px_cap = npx;
+  }
+  rrt_render_params q = *p;
+  if (counters_out) q.flags |= RRT_RENDER_COUNTERS;
+  int rc = launch(c, &q, tiles.data(), nt, ts, x0, y0, x0 + w, y0 + h, c->d_rgb, c->d_cnt,
+                  draws_out ? c->d_draws : nullptr, counters_out ? c->d_ctr : nullptr, c->stream);
+  if (rc) return rc;
+  std::vector<float> rgb(npx * 3);
+  std::vector<int32_t> cnt(npx);
+  std::vector<uint32_t> drw(draws_out ? npx : 0), ctr(counters_out ? npx * 4 : 0);
+  HIPCHK(c, hipMemcpyAsync(rgb.data(), c->d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(cnt.data(), c->d_cnt, npx * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  if (draws_out) HIPCHK(c, hipMemcpyAsync(drw.data(), c->d_draws, npx * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  if (counters_out)
+    HIPCHK(c, hipMemcpyAsync(ctr.data(), c->d_ctr, npx * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t t = 0; t < nt; ++t) {
+    for (uint32_t j = 0; j < ts; ++j) {
+      for (uint32_t i = 0; i < ts; ++i) {
+        uint32_t x = tiles[2 * t] + i, y = tiles[2 * t + 1] + j;
+        if (x >= x0 + w || y >= y0 + h) continue;
+        size_t k = (size_t)t * ts * ts + (size_t)j * ts + i;
+        size_t o = (size_t)(y - y0) * w + (x - x0);
+        rgb_out[3 * o] = rgb[3 * k]; rgb_out[3 * o + 1] = rgb[3 * k + 1]; rgb_out[3 * o + 2] = rgb[3 * k + 2];
+        count_out[o] = cnt[k];
+        if (draws_out) draws_out[o] = drw[k];
+        if (counters_out) std::memcpy(counters_out + 4 * o, &ctr[4 * k], 4 * sizeof(uint32_t));
+      }
+    }
+  }
+  return RRT_OK;
+}
+
+extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
+  rrt_ctx* c = const_cast<rrt_ctx*>(cc);
+  if (!c || !out) return RRT_E_INVALID;
+  std::memset(out, 0, sizeof(*out));
+  out->n_prims = (uint32_t)c->prims.size();
+  out->n_nodes = (uint32_t)c->nodes.size();
+  out->n_leaf_refs = (uint32_t)c->leaf.size();
+  out->max_depth = c->max_depth;
+  out->device_bytes = c->device_bytes;
+  out->grid_blocks = c->last_grid;
+  out->block_threads = 256;
+  if (c->device >= 0 && c->timed) {
+    hipSetDevice(c->device);
+    if (hipEventSynchronize(c->ev1) == hipSuccess) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_ms = ms;
+    }
+  }
+  out->last_kernel_ms = c->last_ms;
+  return RRT_OK;
+}
+
+extern "C" int rrt_get_bvh(const rrt_ctx* c, double* boxes, int32_t* nodes, uint32_t* prims) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  for (size_t i = 0; i < c->nodes.size(); ++i) {
+    const BNode& n = c->nodes[i];
+    if (boxes) {
+      double b[6] = {n.bb.mn.x, n.bb.mn.y, n.bb.mn.z, n.bb.mx.x, n.bb.mx.y, n.bb.mx.z};
+      std::memcpy(boxes + 6 * i, b, sizeof(b));
+    }
+    if (nodes) { nodes[4 * i] = n.first; nodes[4 * i + 1] = n.count; nodes[4 * i + 2] = n.left; nodes[4 * i + 3] = n.right; }
+  }
+  if (prims) std::memcpy(prims, c->leaf.data(), c->leaf.size() * sizeof(uint32_t));
+  return RRT_OK;
+}
+
+// ---------------------------------------------------------------------------- file helpers
+struct rrt_scene_file {
+  std::vector<rrt_object_desc> objects;
+  std::vector<rrt_bsdf_desc> bsdfs;
+  std::vector<rrt_light_desc> lights;
+  std::vector<std::vector<double>> dbl;
+  std::vector<std::vector<uint32_t>> idx;
+  rrt_scene_desc desc{};
+};
+
+static bool rd(FILE* f, void* p, size_t n) { return std::fread(p, 1, n, f) == n; }
+
+extern "C" int rrt_scene_file_load(const char* path, rrt_scene_file** out) {
+  if (!path || !out) return RRT_E_INVALID;
+  *out = nullptr;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return RRT_E_IO;
+  std::unique_ptr<rrt_scene_file> s(new rrt_scene_file());
+  char magic[8];
+  uint32_t hdr[4];
+  bool ok = rd(f, magic, 8) && std::memcmp(magic, RRT_SCENE_MAGIC, 8) == 0 && rd(f, hdr, 16);
+  if (ok) {
+    s->bsdfs.resize(hdr[0]);
+    for (auto& b : s->bsdfs) {
+      uint32_t tp[2];
+      ok = ok && rd(f, tp, 8) && rd(f, b.params, 56);
+      b.type = tp[0];
+    }
+    s->objects.resize(hdr[1]);
+    s->dbl.reserve(2 * hdr[1]);
+    s->idx.reserve(hdr[1]);
+    for (auto& o : s->objects) {
+      if (!ok) break;
+      uint32_t oh[4];
+      ok = rd(f, oh, 16);
+      std::memset(&o, 0, sizeof(o));
+      o.kind = oh[0]; o.bsdf = oh[1];
+      if (ok && oh[0] == RRT_OBJ_MESH) {
+        o.n_vertices = oh[2]; o.n_triangles = oh[3];
+        s->dbl.emplace_back((size_t)oh[2] * 3);
+        s->dbl.emplace_back((size_t)oh[2] * 3);
+        s->idx.emplace_back((size_t)oh[3] * 3);
+        auto& P = s->dbl[s->dbl.size() - 2];
+        auto& N = s->dbl.back();
+        auto& I = s->idx.back();
+        ok = rd(f, P.data(), P.size() * 8) && rd(f, N.data(), N.size() * 8) && rd(f, I.data(), I.size() * 4);
+        o.positions = P.data(); o.normals = N.data(); o.indices = I.data();
+      } else if (ok && oh[0] == RRT_OBJ_SPHERE) {
+        double sp[4];
+        ok = rd(f, sp, 32);
+        o.center[0] = sp[0]; o.center[1] = sp[1]; o.center[2] = sp[2]; o.radius = sp[3];
+      } else {
+        ok = false;
+      }
+    }
+    s->lights.resize(hdr[2]);
+    for (auto& l : s->lights) {
+      if (!ok) break;
+      uint32_t th[2]; float fv[4];
+      ok = rd(f, th, 8) && rd(f, fv, 16) && rd(f, l.v, 96);
+      l.type = th[0]; l.is_delta = th[1];
+      l.radiance[0] = fv[0]; l.radiance[1] = fv[1]; l.radiance[2] = fv[2]; l.area = fv[3];
+    }
+  }
+  std::fclose(f);
+  if (!ok) return RRT_E_IO;
+  s->desc.n_objects = (uint32_t)s->objects.size();
+  s->desc.n_bsdfs = (uint32_t)s->bsdfs.size();
+  s->desc.n_lights = (uint32_t)s->lights.size();
+  s->desc.objects = s->objects.data();
+  s->desc.bsdfs = s->bsdfs.data();
+  s->desc.lights = s->lights.data();
+  *out = s.release();
+  return RRT_OK;
+}
+extern "C" const rrt_scene_desc* rrt_scene_file_desc(const rrt_scene_file* f) { return f ? &f->desc : nullptr; }
+extern "C" void rrt_scene_file_free(rrt_scene_file* f) { delete f; }
+
+extern "C" int rrt_camera_file_load(const char* path, rrt_camera_desc* out) {
+  if (!path || !out) return RRT_E_INVALID;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return RRT_E_IO;
+  char magic[8];
+  double d[RRT_CAMERA_NDOUBLES];
+  bool ok = rd(f, magic, 8) && std::memcmp(magic, RRT_CAMERA_MAGIC, 8) == 0 && rd(f, d, sizeof(d));
+  std::fclose(f);
+  if (!ok) return RRT_E_IO;
+  std::memset(out, 0, sizeof(*out));
+  out->hFov = d[0]; out->vFov = d[1]; out->nClip = d[3]; out->fClip = d[4];
+  for (int i = 0; i < 3; ++i) out->pos[i] = d[5 + i];
+  std::memcpy(out->c2w, d + 16, 9 * sizeof(double));
+  out->focalDistance = d[28]; out->lensRadius = d[29];
+  return RRT_OK;
+}

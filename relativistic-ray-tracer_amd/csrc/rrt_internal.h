@@ -1,0 +1,86 @@
+// rrt_internal.h -- device data layout shared by the host side (rrt_host.cpp) and the
+// kernels (rrt_kernel.hip).  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+#define RRT_MAX_LIGHTS 16
+#define RRT_MAX_BSDFS 64
+#define RRT_MAX_DEPTH 16
+
+// BVH node, 64 B, left-first pre-order (the reference's recursion order, bvh.cpp:115-138).
+// Left child of an inner node is always index + 1; `skip` is the pre-order successor of the
+// whole subtree, so "bbox missed or leaf done -> skip, else -> index + 1" visits exactly the
+// nodes the reference's left-then-right recursion visits, in the same order, with no stack.
+struct alignas(16) DNode {
+  double mn[3];
+  double mx[3];
+  int32_t skip;    // next node after this subtree (-1: done)
+  int32_t first;   // leaf: first slot in the leaf arrays
+  int32_t count;   // leaf: number of slots (0: inner node)
+  int32_t pad;
+};
+static_assert(sizeof(DNode) == 64, "DNode must be 64 bytes");
+
+// Leaf-slot geometry, 72 B (9 doubles) per slot, slots in leaf order.
+//   triangle: p0, e1 = p1 - p0, e2 = p2 - p0 (exactly the values triangle.cpp:31-32 computes)
+//   sphere:   c.x, c.y, c.z, r2, r, 0...
+struct DPrimGeo { double v[9]; };
+// Leaf-slot shading data: vertex normals n0, n1, n2 (triangle) -- read only on an accepted hit.
+struct DPrimNrm { double n[9]; };
+// Leaf-slot metadata: bit 0 = sphere, bits 8..15 = bsdf index.
+typedef uint32_t DPrimMeta;
+
+struct DBsdf {
+  uint32_t type;
+  float p[14];
+};
+struct DLight {
+  uint32_t type, is_delta;
+  float rad[3];
+  float area;
+  double v[4][3];
+};
+
+struct DCamera {
+  double pos[3];
+  double c2w0[3], c2w1[3], c2w2[3];   // columns
+  double blx, bly;                     // -tan(radians(fov)/2), host libm (part1_code.cpp:183)
+};
+struct DHole {
+  double c[3];
+  double r, r2, dt, cos_dt, sin_dt;    // cos/sin(dt) from host libm (blackhole.cpp:36-37)
+  int32_t steps;                        // #{j : j * dt < 2 pi}  (bvh.cpp:105)
+  int32_t pad;
+};
+
+struct KParams {
+  // scene
+  const DNode* nodes;
+  const DPrimGeo* geo;
+  const DPrimNrm* nrm;
+  const DPrimMeta* meta;
+  const DBsdf* bsdfs;
+  const DLight* lights;
+  uint32_t n_lights;
+  uint32_t pad0;
+  DCamera cam;
+  DHole hole;
+  // render
+  uint32_t ns_aa, max_ray_depth, ns_area_light, samples_per_batch;
+  float max_tolerance;
+  uint32_t direct_hemisphere;
+  uint64_t seed;
+  double frame_w, frame_h;
+  uint32_t frame_wi, frame_hi;
+  // work: list of tiles (x, y), each split into 8x8 pixel blocks pulled by waves
+  const uint32_t* tiles;
+  uint32_t n_tiles, tile_size;
+  uint32_t blocks_per_tile_side, n_blocks;
+  uint32_t* block_counter;
+  uint32_t clip_x0, clip_y0, clip_x1, clip_y1;  // region actually requested (exclusive end)
+  // outputs, packed per tile: pixel (i, j) of tile t at t*tile_size^2 + j*tile_size + i
+  float* rgb;
+  int32_t* count;
+  uint32_t* draws;      // optional
+  uint32_t* counters;   // optional [4] per pixel
+};

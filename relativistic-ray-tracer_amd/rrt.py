@@ -1,0 +1,224 @@
+"""ctypes binding of librrt.so (include/rrt.h) -- the host-side mirror of the reference's
+PathTracer hot-path interface for Python callers (tests, bench, smoke).
+
+The product path is native: librrt.so (HIP kernels + C ABI).  This module only marshals
+arguments; it never computes radiance itself and raises if the library is missing.
+
+Reference correspondence (pathtracer.h / pathtracer.cpp):
+    Renderer(device)                  PathTracer ctor (pathtracer.cpp:32-85)
+    .set_scene(SceneFile)             PathTracer::set_scene + build_accel (:95-117, :304-328)
+    .set_camera(camera)               PathTracer::set_camera (:119-134)
+    .set_black_hole(c, r_s, dtheta)   the `-B` override of global_black_hole (main.cpp:139-145)
+    .render(params, x0, y0, w, h)     raytrace_tile / raytrace_cell over a region (:549-609)
+    RenderParams(...)                 AppConfig fields (application.h:41-85)
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librrt.so")
+
+RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
+RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS = 1, 2
+
+
+class RRTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rrt error {code}: {msg}")
+        self.code = code
+
+
+class DeviceCfg(C.Structure):
+    _fields_ = [("device", C.c_int), ("reserved", C.c_uint32 * 7)]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [("hFov", C.c_double), ("vFov", C.c_double), ("nClip", C.c_double), ("fClip", C.c_double),
+                ("pos", C.c_double * 3), ("c2w", C.c_double * 9), ("lensRadius", C.c_double),
+                ("focalDistance", C.c_double)]
+
+
+class SpacetimeDesc(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("center", C.c_double * 3), ("r_s", C.c_double),
+                ("delta_theta", C.c_double)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("ns_aa", C.c_uint32), ("max_ray_depth", C.c_uint32), ("ns_area_light", C.c_uint32),
+                ("samples_per_batch", C.c_uint32), ("max_tolerance", C.c_float),
+                ("direct_hemisphere", C.c_uint32), ("seed", C.c_uint64), ("frame_w", C.c_uint32),
+                ("frame_h", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_prims", C.c_uint32), ("n_nodes", C.c_uint32), ("n_leaf_refs", C.c_uint32),
+                ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("last_kernel_ms", C.c_float),
+                ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32)]
+
+
+# every symbol include/rrt.h declares (checked by tests/test_capi_host.py)
+EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
+           "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
+           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_bvh",
+           "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load"]
+
+_lib = None
+
+
+def lib():
+    """Load librrt.so (fails loudly if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RRTError(RRT_E_IO, f"{LIB_PATH} not built (run `make -C relativistic-ray-tracer_amd`)")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.rrt_create.argtypes = [C.POINTER(vp), C.POINTER(DeviceCfg)]
+        L.rrt_destroy.argtypes = [vp]
+        L.rrt_last_error.restype = C.c_char_p
+        L.rrt_last_error.argtypes = [vp]
+        L.rrt_set_scene.argtypes = [vp, vp]
+        L.rrt_set_camera.argtypes = [vp, C.POINTER(CameraDesc)]
+        L.rrt_set_spacetime.argtypes = [vp, C.POINTER(SpacetimeDesc)]
+        L.rrt_render_params_default.argtypes = [C.POINTER(RenderParams)]
+        L.rrt_render.argtypes = [vp, C.POINTER(RenderParams), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp,
+                                 vp, vp, vp]
+        L.rrt_render_tiles_device.argtypes = [vp, C.POINTER(RenderParams), vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+        L.rrt_unpack_tiles_device.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp,
+                                              vp]
+        L.rrt_tonemap_device.argtypes = [vp, C.c_uint32, vp, vp, vp]
+        L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
+        L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
+        L.rrt_scene_file_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.rrt_scene_file_desc.restype = vp
+        L.rrt_scene_file_desc.argtypes = [vp]
+        L.rrt_scene_file_free.argtypes = [vp]
+        L.rrt_camera_file_load.argtypes = [C.c_char_p, C.POINTER(CameraDesc)]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class SceneFile:
+    """A flattened static scene (.rrts, include/rrt_scene_format.h) loaded by librrt."""
+
+    def __init__(self, path):
+        h = C.c_void_p()
+        rc = lib().rrt_scene_file_load(path.encode(), C.byref(h))
+        if rc != RRT_OK:
+            raise RRTError(rc, f"cannot load scene {path}")
+        self.h = h
+
+    def desc(self):
+        return lib().rrt_scene_file_desc(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rrt_scene_file_free(self.h)
+            self.h = None
+
+
+def load_camera(path):
+    cam = CameraDesc()
+    rc = lib().rrt_camera_file_load(path.encode(), C.byref(cam))
+    if rc != RRT_OK:
+        raise RRTError(rc, f"cannot load camera {path}")
+    return cam
+
+
+def render_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
+                  max_tolerance=0.05, direct_hemisphere=False, seed=0, flags=0):
+    p = RenderParams()
+    lib().rrt_render_params_default(C.byref(p))
+    p.ns_aa, p.max_ray_depth, p.ns_area_light = ns_aa, max_ray_depth, ns_area_light
+    p.samples_per_batch, p.max_tolerance, p.direct_hemisphere = samples_per_batch, max_tolerance, int(direct_hemisphere)
+    p.seed, p.frame_w, p.frame_h, p.flags = seed, frame_w, frame_h, flags
+    return p
+
+
+def partition_tiles(frame_w, frame_h, tile_size, rank, world):
+    n = lib().rrt_partition_tiles(frame_w, frame_h, tile_size, rank, world, None, 0)
+    if n < 0:
+        raise RRTError(n, "bad partition arguments")
+    out = np.zeros((max(n, 1), 2), np.uint32)
+    lib().rrt_partition_tiles(frame_w, frame_h, tile_size, rank, world, out.ctypes.data, n)
+    return out[:n]
+
+
+class Renderer:
+    """One rendering context on one HIP device (device=-1: host-only, for BVH/host tests)."""
+
+    def __init__(self, device=0):
+        cfg = DeviceCfg()
+        cfg.device = device
+        h = C.c_void_p()
+        rc = lib().rrt_create(C.byref(h), C.byref(cfg))
+        if rc != RRT_OK:
+            raise RRTError(rc, f"rrt_create(device={device}) failed")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rrt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _chk(self, rc):
+        if rc != RRT_OK:
+            raise RRTError(rc, lib().rrt_last_error(self.h).decode())
+
+    def set_scene(self, scene_file):
+        self._scene = scene_file
+        self._chk(lib().rrt_set_scene(self.h, scene_file.desc()))
+
+    def set_camera(self, cam):
+        self._chk(lib().rrt_set_camera(self.h, C.byref(cam)))
+
+    def set_black_hole(self, center=(0.0, 1.0, 0.0), r_s=0.1, delta_theta=0.1):
+        st = SpacetimeDesc()
+        st.kind = 0
+        st.center[0], st.center[1], st.center[2] = center
+        st.r_s, st.delta_theta = r_s, delta_theta
+        self._chk(lib().rrt_set_spacetime(self.h, C.byref(st)))
+
+    def render(self, params, x0, y0, w, h, draws=False, counters=False):
+        rgb = np.zeros((h, w, 3), np.float32)
+        cnt = np.zeros((h, w), np.int32)
+        dr = np.zeros((h, w), np.uint32) if draws else None
+        ct = np.zeros((h, w, 4), np.uint32) if counters else None
+        self._chk(lib().rrt_render(self.h, C.byref(params), x0, y0, w, h, _p(rgb), _p(cnt), _p(dr), _p(ct), None))
+        return rgb, cnt, dr, ct
+
+    def render_tiles_device(self, params, tiles, tile_size, d_rgb, d_count, d_counters=None, stream=None):
+        tiles = np.ascontiguousarray(tiles, dtype=np.uint32)
+        self._chk(lib().rrt_render_tiles_device(self.h, C.byref(params), _p(tiles), len(tiles), tile_size, d_rgb,
+                                                d_count, d_counters, stream))
+
+    def unpack_tiles_device(self, tiles, tile_size, frame_w, frame_h, rgb_p, cnt_p, rgb, cnt, stream=None):
+        tiles = np.ascontiguousarray(tiles, dtype=np.uint32)
+        self._chk(lib().rrt_unpack_tiles_device(self.h, _p(tiles), len(tiles), tile_size, frame_w, frame_h, rgb_p,
+                                                cnt_p, rgb, cnt, stream))
+
+    def tonemap_device(self, n, d_rgb, d_rgba, stream=None):
+        self._chk(lib().rrt_tonemap_device(self.h, n, d_rgb, d_rgba, stream))
+
+    def stats(self):
+        s = Stats()
+        self._chk(lib().rrt_get_stats(self.h, C.byref(s)))
+        return s
+
+    def bvh(self):
+        s = self.stats()
+        boxes = np.zeros((s.n_nodes, 6), np.float64)
+        nodes = np.zeros((s.n_nodes, 4), np.int32)
+        prims = np.zeros(s.n_leaf_refs, np.uint32)
+        self._chk(lib().rrt_get_bvh(self.h, _p(boxes), _p(nodes), _p(prims)))
+        return boxes, nodes, prims

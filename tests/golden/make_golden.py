@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the REFERENCE renderer itself.
+
+TEST INFRASTRUCTURE ONLY.  Runs in the build container (needs /root/reference); the GPU box
+only ever reads the fixtures this writes.  Steps:
+
+  1. `make -C oracle/ref` compiles the reference's own sources (oracle/ref/Makefile) into
+     oracle/_ref/{ref_render,ref_kat} (git-ignored).
+  2. ref_kat  -> tests/golden/kat/kat_<family>.npz   (function-level known answers)
+  3. ref_render for every case in CASES -> tests/golden/scenes/<dae>.rrts (+ _bvh.npz: the
+     reference BVH in left-first pre-order, for the BVH-builder tests) and tests/golden/<case>/
+        camera.rrtc                camera record (include/rrt_scene_format.h)
+        px.npz                     per-pixel RGB (f32), sample count, RNG draw count
+                                   (+ AABB-test / micro-step counters for small cases)
+        case.json                  the reference command line and render parameters
+
+The keyed per-pixel RNG (oracle/ref/harness_common.h) makes every pixel independent of the
+thread schedule; step 4 re-renders one case with -t 1 and asserts bit-identity with -t 8.
+
+Usage:  python3 tests/golden/make_golden.py [--only NAME ...] [--jobs 8]
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+GOLD = os.path.join(ROOT, "tests", "golden")
+REF = "/root/reference/pathtracer"
+DAE = os.path.join(REF, "dae", "sky")
+BIN = os.path.join(ROOT, "oracle", "_ref")
+
+# name -> (dae, args, keep_counters)
+# Reference defaults (application.h:45-62): -s 1 -l 1 -m 1 -t 1, batch 32, tol 0.05; default
+# black hole (blackhole.cpp:5) centre (0,1,0), r_s 0.1, dtheta 0.1.
+CASES = {
+    # BASELINE configs
+    "cfg1_spheres_480x360_s8": ("CBspheres_lambertian.dae", ["-s", "8", "-r", "480", "360"], False),
+    "cfg2_spheres_1080p_s64_flat": ("CBspheres_lambertian.dae",
+                                    ["-s", "64", "-r", "1920", "1080", "-B", "0", "1", "0", "0", "0.1"], False),
+    "cfg3_bunny_1080p_s64": ("CBbunny.dae", ["-s", "64", "-r", "1920", "1080"], False),
+    # small coverage cases (full frames, with per-pixel work counters)
+    "bunny_160x120_s16": ("CBbunny.dae", ["-s", "16", "-r", "160", "120"], True),
+    "spheres_96x72_s1": ("CBspheres_lambertian.dae", ["-s", "1", "-r", "96", "72"], True),
+    "spheres_96x72_s40_m3": ("CBspheres_lambertian.dae", ["-s", "40", "-m", "3", "-r", "96", "72"], True),
+    "spheres_96x72_s8_l4": ("CBspheres_lambertian.dae", ["-s", "8", "-l", "4", "-r", "96", "72"], True),
+    "spheres_96x72_s8_hemi": ("CBspheres_lambertian.dae", ["-s", "8", "-H", "-r", "96", "72"], True),
+    "spheres_96x72_s64_a16": ("CBspheres_lambertian.dae", ["-s", "64", "-a", "16", "0.2", "-r", "96", "72"], True),
+    "spheres_96x72_s8_m0": ("CBspheres_lambertian.dae", ["-s", "8", "-m", "0", "-r", "96", "72"], True),
+    "spheres_bh_96x72_s8": ("CBspheres_lambertian.dae",
+                            ["-s", "8", "-r", "96", "72", "-B", "0.1", "0.8", "-0.1", "0.3", "0.05"], True),
+    "glass_mirror_96x72_s16_m4": ("CBspheres.dae", ["-s", "16", "-m", "4", "-r", "96", "72"], True),
+    "microfacet_96x72_s16_m2": ("CBspheres_microfacet_al_ag.dae", ["-s", "16", "-m", "2", "-r", "96", "72"], True),
+    "coil_96x72_s8": ("CBcoil.dae", ["-s", "8", "-r", "96", "72"], True),
+    "gems_96x72_s8_m3": ("CBgems.dae", ["-s", "8", "-m", "3", "-r", "96", "72"], True),
+    "empty_64x48_s8": ("CBempty.dae", ["-s", "8", "-r", "64", "48"], True),
+    "bunnycu_96x72_s8_m2": ("CBbunny_microfacet_cu.dae", ["-s", "8", "-m", "2", "-r", "96", "72"], True),
+    # a crop in cell mode (-p x y dx dy; y in sampleBuffer coordinates, y = 0 at the bottom)
+    "bunny_1080p_s64_crop": ("CBbunny.dae", ["-s", "64", "-r", "1920", "1080", "-p", "896", "476", "96", "96"], True),
+}
+
+
+def run(cmd, **kw):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, **kw)
+
+
+def render(dae, args, workdir, threads, seed=0):
+    prefix = os.path.join(workdir, "ref")
+    cmd = [os.path.join(BIN, "ref_render"), "-t", str(threads), "-S", str(seed), "-O", prefix,
+           "-f", os.path.join(workdir, "out.png")] + args + [os.path.join(DAE, dae)]
+    run(cmd, stdout=subprocess.DEVNULL)
+    return prefix
+
+
+def load_px(prefix, counters):
+    d = {k: np.load(f"{prefix}_px_{k}.npy") for k in ("rgb", "count", "draws", "meta")}
+    if counters:
+        d["bbox_tests"] = np.load(f"{prefix}_px_bbox_tests.npy")
+        d["micro_steps"] = np.load(f"{prefix}_px_micro_steps.npy")
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--skip-build", action="store_true")
+    a = ap.parse_args()
+
+    if not a.skip_build:
+        run(["make", "-C", os.path.join(ROOT, "oracle", "ref"), f"-j{a.jobs}"])
+
+    if not a.only or "kat" in a.only:
+        kdir = os.path.join(GOLD, "kat")
+        os.makedirs(kdir, exist_ok=True)
+        with tempfile.TemporaryDirectory() as td:
+            run([os.path.join(BIN, "ref_kat"), td])
+            for f in sorted(os.listdir(td)):
+                arr = np.load(os.path.join(td, f))
+                np.savez_compressed(os.path.join(kdir, f.replace(".npy", ".npz")), v=arr)
+
+    for name, (dae, args, counters) in CASES.items():
+        if a.only and name not in a.only:
+            continue
+        out = os.path.join(GOLD, name)
+        os.makedirs(out, exist_ok=True)
+        with tempfile.TemporaryDirectory() as td:
+            prefix = render(dae, args, td, a.jobs)
+            # scenes (and their reference BVH) are shared between cases of the same .dae
+            sdir = os.path.join(GOLD, "scenes")
+            os.makedirs(sdir, exist_ok=True)
+            stem = dae.replace(".dae", "")
+            spath = os.path.join(sdir, stem + ".rrts")
+            with open(prefix + ".rrts", "rb") as f:
+                sbytes = f.read()
+            if os.path.exists(spath):
+                with open(spath, "rb") as f:
+                    assert f.read() == sbytes, f"scene dump of {dae} changed between cases"
+            else:
+                with open(spath, "wb") as f:
+                    f.write(sbytes)
+                np.savez_compressed(os.path.join(sdir, stem + "_bvh.npz"),
+                                    boxes=np.load(prefix + "_bvh_boxes.npy"),
+                                    nodes=np.load(prefix + "_bvh_nodes.npy"),
+                                    prims=np.load(prefix + "_bvh_prims.npy"))
+            shutil.copy(prefix + ".rrtc", os.path.join(out, "camera.rrtc"))
+            px = load_px(prefix, counters)
+            np.savez_compressed(os.path.join(out, "px.npz"), **px)
+        meta = px["meta"]
+        info = {
+            "dae": dae, "scene": "scenes/" + dae.replace(".dae", "") + ".rrts", "args": args,
+            "seed": 0, "threads": a.jobs,
+            "region": {"x0": int(meta[0]), "y0": int(meta[1]), "w": int(meta[2]), "h": int(meta[3])},
+            "frame": {"w": int(meta[4]), "h": int(meta[5])},
+            "samples": int(px["count"].astype(np.int64).sum()),
+            "nonblack_fraction": float((px["rgb"].sum(-1) > 0).mean()),
+        }
+        if counters:
+            info["bbox_tests"] = int(px["bbox_tests"].astype(np.int64).sum())
+            info["micro_steps"] = int(px["micro_steps"].astype(np.int64).sum())
+            info["prim_tests_total"] = int(meta[7])
+        with open(os.path.join(out, "case.json"), "w") as f:
+            json.dump(info, f, indent=1)
+        print(name, info, flush=True)
+
+    # 4. schedule independence: -t 1 must reproduce -t 8 bit for bit
+    if not a.only or "determinism" in a.only:
+        dae, args, _ = CASES["spheres_96x72_s40_m3"]
+        with tempfile.TemporaryDirectory() as td:
+            p1 = load_px(render(dae, args, td, 1), True)
+            ref = np.load(os.path.join(GOLD, "spheres_96x72_s40_m3", "px.npz"))
+            for k in ("rgb", "count", "draws", "bbox_tests", "micro_steps"):
+                assert np.array_equal(p1[k], ref[k]), f"-t 1 differs from -t {a.jobs} in {k}"
+            # with one thread the reference's own (racy) total_isects counter is exact
+            with open(os.path.join(GOLD, "spheres_96x72_s40_m3", "case.json")) as f:
+                info = json.load(f)
+            info["prim_tests_total"] = int(p1["meta"][7])
+            with open(os.path.join(GOLD, "spheres_96x72_s40_m3", "case.json"), "w") as f:
+                json.dump(info, f, indent=1)
+        print("determinism: -t 1 == -t", a.jobs, "(bit-identical)")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

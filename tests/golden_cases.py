@@ -1,0 +1,75 @@
+"""Golden cases produced by tests/golden/make_golden.py from the reference renderer."""
+import json
+import os
+
+import numpy as np
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def parse_args(args):
+    """Reference CLI flags (main.cpp:88-145) -> render settings."""
+    cfg = dict(ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32, max_tolerance=0.05,
+               direct_hemisphere=False, bh=(0.0, 1.0, 0.0, 0.1, 0.1))
+    i = 0
+    while i < len(args):
+        a = args[i]
+        if a == "-s": cfg["ns_aa"] = int(args[i + 1]); i += 2
+        elif a == "-m": cfg["max_ray_depth"] = int(args[i + 1]); i += 2
+        elif a == "-l": cfg["ns_area_light"] = int(args[i + 1]); i += 2
+        elif a == "-H": cfg["direct_hemisphere"] = True; i += 1
+        elif a == "-a": cfg["samples_per_batch"] = int(args[i + 1]); cfg["max_tolerance"] = float(args[i + 2]); i += 3
+        elif a == "-B": cfg["bh"] = tuple(float(v) for v in args[i + 1:i + 6]); i += 6
+        elif a == "-r": i += 3
+        elif a == "-p": i += 5
+        else: raise ValueError(f"unhandled flag {a}")
+    return cfg
+
+
+class Case:
+    def __init__(self, name):
+        self.name = name
+        self.dir = os.path.join(GOLD, name)
+        with open(os.path.join(self.dir, "case.json")) as f:
+            self.info = json.load(f)
+        self.cfg = parse_args(self.info["args"])
+        self.scene_path = os.path.join(GOLD, self.info["scene"])
+        self.camera_path = os.path.join(self.dir, "camera.rrtc")
+        self.frame_w, self.frame_h = self.info["frame"]["w"], self.info["frame"]["h"]
+        r = self.info["region"]
+        self.x0, self.y0, self.w, self.h = r["x0"], r["y0"], r["w"], r["h"]
+        self._px = None
+
+    @property
+    def px(self):
+        if self._px is None:
+            self._px = dict(np.load(os.path.join(self.dir, "px.npz")))
+        return self._px
+
+    @property
+    def exact(self):
+        """Cases whose hot path has no per-sample transcendental (the keyed draws feed only
+        + - * / sqrt): the GPU must match bit for bit.  Bounces (cos/sin), the hemisphere
+        sampler (acos/sinf/cosf) and microfacet/glass BSDFs use the device libm."""
+        c = self.cfg
+        return c["max_ray_depth"] <= 1 and not c["direct_hemisphere"]
+
+
+def all_cases():
+    return sorted(d for d in os.listdir(GOLD) if os.path.exists(os.path.join(GOLD, d, "case.json")))
+
+
+SMALL = [c for c in all_cases() if not c.startswith(("cfg2", "cfg3"))] if os.path.isdir(GOLD) else []
+
+
+def parity_metrics(ref_rgb, got_rgb):
+    """SURVEY 8(c) tolerance statement: RMS over pixels of |dRGB|_2, also over non-black pixels."""
+    d = np.linalg.norm(got_rgb.astype(np.float64) - ref_rgb.astype(np.float64), axis=-1)
+    nb = ref_rgb.sum(-1) > 0
+    return {
+        "rms": float(np.sqrt(np.mean(d ** 2))),
+        "rms_nonblack": float(np.sqrt(np.mean(d[nb] ** 2))) if nb.any() else 0.0,
+        "max": float(d.max()),
+        "bit_exact_frac": float(np.mean((got_rgb == ref_rgb).all(-1))),
+        "outliers_1e-3": int((d > 1e-3).sum()),
+    }

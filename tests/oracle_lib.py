@@ -1,0 +1,128 @@
+"""ctypes binding of the CPU restatement (oracle/restate/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg -- never by the product path.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+LIB_DIR = os.path.join(ROOT, "oracle", "restate")
+LIB_PATH = os.path.join(LIB_DIR, "liboracle.so")
+
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+class Camera(C.Structure):
+    _fields_ = [("hFov", C.c_double), ("vFov", C.c_double), ("nClip", C.c_double), ("fClip", C.c_double),
+                ("pos", C.c_double * 3), ("c2w", C.c_double * 9), ("lensRadius", C.c_double),
+                ("focalDistance", C.c_double)]
+
+
+class Params(C.Structure):
+    _fields_ = [("ns_aa", C.c_uint32), ("max_ray_depth", C.c_uint32), ("ns_area_light", C.c_uint32),
+                ("samples_per_batch", C.c_uint32), ("max_tolerance", C.c_float),
+                ("direct_hemisphere", C.c_uint32), ("seed", C.c_uint64), ("frame_w", C.c_uint32),
+                ("frame_h", C.c_uint32), ("bh_center", C.c_double * 3), ("bh_radius", C.c_double),
+                ("bh_dtheta", C.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-C", LIB_DIR], check=True, stdout=subprocess.DEVNULL)
+        L = C.CDLL(LIB_PATH)
+        L.ro_scene_load.restype = C.c_void_p
+        L.ro_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.ro_scene_free.argtypes = [C.c_void_p]
+        L.ro_scene_num_prims.argtypes = [C.c_void_p]
+        L.ro_scene_num_nodes.argtypes = [C.c_void_p]
+        L.ro_scene_bvh.argtypes = [C.c_void_p, _f64p, _i32p, _u32p]
+        L.ro_camera_load.argtypes = [C.c_char_p, C.POINTER(Camera), C.c_char_p, C.c_int]
+        L.ro_params_default.argtypes = [C.POINTER(Params)]
+        L.ro_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_uint32, C.c_uint32,
+                                C.c_uint32, C.c_uint32, _f32p, _i32p, C.c_void_p, C.c_void_p, C.c_int]
+        L.ro_pixel_key.restype = C.c_uint64
+        L.ro_pixel_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.ro_keyed_rand.argtypes = [C.c_uint64, C.c_uint32]
+        L.ro_micro_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int]
+        L.ro_bbox_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_double, C.c_double,
+                                        C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.ro_tri_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.POINTER(C.c_double), _f64p, _f64p]
+        L.ro_sphere_intersect.argtypes = [_f64p, C.c_double, _f64p, _f64p, C.POINTER(C.c_double), _f64p,
+                                          _f64p, C.c_int]
+        L.ro_coord_space.argtypes = [_f64p, _f64p, _f64p, _f64p, _f64p]
+        L.ro_sampler.argtypes = [C.c_int, _i32p, _f64p, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.ro_bsdf_sample.argtypes = [C.c_int, _f64p, _f64p, _i32p, _f32p, _f64p, C.POINTER(C.c_float),
+                                     C.POINTER(C.c_int), _f32p]
+        L.ro_area_sample.argtypes = [_f32p, _f64p, _f64p, _i32p, _f32p, _f64p, C.POINTER(C.c_float),
+                                     C.POINTER(C.c_float)]
+        L.ro_camera_ray.argtypes = [C.c_double, C.c_double, _f64p, _f64p, C.c_double, C.c_double, C.c_double,
+                                    C.c_double, _f64p, _f64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+class Scene:
+    def __init__(self, path):
+        err = C.create_string_buffer(256)
+        self.h = lib().ro_scene_load(path.encode(), err, 256)
+        if not self.h:
+            raise RuntimeError(err.value.decode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ro_scene_free(self.h)
+            self.h = None
+
+    def bvh(self):
+        n = lib().ro_scene_num_nodes(self.h)
+        p = lib().ro_scene_num_prims(self.h)
+        boxes = np.zeros((n, 6), np.float64)
+        nodes = np.zeros((n, 4), np.int32)
+        prims = np.zeros(p, np.uint32)
+        lib().ro_scene_bvh(self.h, boxes, nodes, prims)
+        return boxes, nodes, prims
+
+
+def load_camera(path):
+    cam = Camera()
+    err = C.create_string_buffer(256)
+    if lib().ro_camera_load(path.encode(), C.byref(cam), err, 256) != 0:
+        raise RuntimeError(err.value.decode())
+    return cam
+
+
+def make_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
+                max_tolerance=0.05, direct_hemisphere=False, seed=0, bh=(0.0, 1.0, 0.0, 0.1, 0.1)):
+    p = Params()
+    lib().ro_params_default(C.byref(p))
+    p.ns_aa, p.max_ray_depth, p.ns_area_light = ns_aa, max_ray_depth, ns_area_light
+    p.samples_per_batch, p.max_tolerance = samples_per_batch, max_tolerance
+    p.direct_hemisphere, p.seed, p.frame_w, p.frame_h = int(direct_hemisphere), seed, frame_w, frame_h
+    p.bh_center[0], p.bh_center[1], p.bh_center[2] = bh[0], bh[1], bh[2]
+    p.bh_radius, p.bh_dtheta = bh[3], bh[4]
+    return p
+
+
+def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):
+    threads = threads or os.cpu_count() or 1
+    rgb = np.zeros((h, w, 3), np.float32)
+    cnt = np.zeros((h, w), np.int32)
+    draws = np.zeros((h, w), np.uint32)
+    ctr = np.zeros((h, w, 4), np.uint32) if counters else None
+    rc = lib().ro_render(scene.h, C.byref(cam), C.byref(params), x0, y0, w, h, rgb, cnt,
+                         draws.ctypes.data, ctr.ctypes.data if counters else None, threads)
+    if rc != 0:
+        raise RuntimeError("ro_render failed")
+    return rgb, cnt, draws, ctr

@@ -1,0 +1,118 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden outputs.
+
+Tolerance (north star): per-pixel L2 of linear HDR RGB, RMS over pixels <= 1e-4, and the same
+RMS over non-black pixels only.  Cases whose hot path uses no per-sample transcendental
+(Case.exact: depth <= 1, importance-sampled direct light) must be bit-exact, including the
+per-pixel sample counts and RNG draw counts."""
+import os
+
+import numpy as np
+import pytest
+
+import rrt
+from golden_cases import SMALL, Case, parity_metrics
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    r = rrt.Renderer(device=0)
+    yield r
+    r.close()
+
+
+def render(gpu, c, draws=True, counters=False):
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    bh = c.cfg["bh"]
+    gpu.set_black_hole(bh[:3], bh[3], bh[4])
+    g = c.cfg
+    p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                          ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                          max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"])
+    return gpu.render(p, c.x0, c.y0, c.w, c.h, draws=draws, counters=counters)
+
+
+def check(c, rgb, cnt, draws):
+    m = parity_metrics(c.px["rgb"], rgb)
+    print(c.name, m, "count_eq", float(np.mean(cnt == c.px["count"])))
+    if c.exact:
+        assert np.array_equal(rgb.view(np.uint32), c.px["rgb"].view(np.uint32)), m
+        assert np.array_equal(cnt, c.px["count"])
+        if draws is not None:
+            assert np.array_equal(draws, c.px["draws"])
+    else:
+        assert m["rms"] <= TOL and m["rms_nonblack"] <= TOL, m
+        assert np.mean(cnt == c.px["count"]) > 0.99
+    return m
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_small_cases(gpu, name):
+    c = Case(name)
+    rgb, cnt, draws, _ = render(gpu, c)
+    check(c, rgb, cnt, draws)
+
+
+@pytest.mark.parametrize("name", ["cfg1_spheres_480x360_s8", "cfg2_spheres_1080p_s64_flat", "cfg3_bunny_1080p_s64"])
+def test_baseline_frames(gpu, name):
+    """The BASELINE.json configs, full frames, bit-exact against the reference."""
+    c = Case(name)
+    rgb, cnt, draws, _ = render(gpu, c)
+    check(c, rgb, cnt, draws)
+
+
+def test_work_counters_closest_hit(gpu):
+    """Counting variant: micro steps per pixel equal the reference's own (camera rays are
+    closest-hit; shadow rays stop at the first hit on the GPU, so AABB tests are <= ref)."""
+    c = Case("spheres_96x72_s1")
+    rgb, cnt, draws, ctr = render(gpu, c, counters=True)
+    assert np.array_equal(rgb.view(np.uint32), c.px["rgb"].view(np.uint32))
+    assert np.all(ctr[..., 0] <= c.px["bbox_tests"])
+    assert np.all(ctr[..., 1] <= c.px["micro_steps"])
+    assert ctr[..., 0].sum() > 0.5 * c.px["bbox_tests"].sum()
+
+
+def test_device_tiles_path_matches_host_path(gpu):
+    """rrt_render_tiles_device (packed tiles) + rrt_unpack_tiles_device == rrt_render."""
+    torch = pytest.importorskip("torch")
+    c = Case("bunny_160x120_s16")
+    rgb_h, cnt_h, _, _ = render(gpu, c, draws=False)
+    W, H, ts = c.frame_w, c.frame_h, 32
+    g = c.cfg
+    p = rrt.render_params(W, H, ns_aa=g["ns_aa"])
+    out_rgb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    out_cnt = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    for world in (1, 3):
+        out_rgb.zero_(); out_cnt.zero_()
+        for r in range(world):
+            tiles = rrt.partition_tiles(W, H, ts, r, world)
+            prgb = torch.zeros(len(tiles) * ts * ts * 3, dtype=torch.float32, device="cuda")
+            pcnt = torch.zeros(len(tiles) * ts * ts, dtype=torch.int32, device="cuda")
+            s = torch.cuda.current_stream().cuda_stream
+            gpu.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+            gpu.unpack_tiles_device(tiles, ts, W, H, prgb.data_ptr(), pcnt.data_ptr(), out_rgb.data_ptr(),
+                                    out_cnt.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        assert np.array_equal(out_rgb.cpu().numpy().reshape(H, W, 3).view(np.uint32), rgb_h.view(np.uint32))
+        assert np.array_equal(out_cnt.cpu().numpy().reshape(H, W), cnt_h)
+
+
+def test_tonemap(gpu):
+    torch = pytest.importorskip("torch")
+    c = Case("cfg1_spheres_480x360_s8")
+    rgb = torch.from_numpy(c.px["rgb"].reshape(-1).copy()).cuda()
+    out = torch.zeros(c.w * c.h, dtype=torch.int32, device="cuda")
+    gpu.tonemap_device(c.w * c.h, rgb.data_ptr(), out.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(c.h, c.w)
+    # HDRImageBuffer::toColor + ImageBuffer::update_pixel (image.h:53-62, 183-198), float pow
+    s = c.px["rgb"].astype(np.float32) * np.float32(np.sqrt(2.0))
+    v = np.power(s, np.float32(1.0) / np.float32(2.2)).astype(np.float32)
+    v = np.where(v < 1, v, np.float32(1)).astype(np.float32)
+    q = (v * np.float32(255)).astype(np.uint32)
+    want = 0xFF000000 | (q[..., 2] << 16) | (q[..., 1] << 8) | q[..., 0]
+    diff = np.abs(((got >> 0) & 255).astype(int) - (want & 255).astype(int))
+    assert diff.max() <= 1 and np.mean(got == want) > 0.999
