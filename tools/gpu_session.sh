@@ -1,0 +1,29 @@
+#!/bin/bash
+# One gpurun session: every GPU step under its own time limit; stop at the first fault /
+# abort / timeout (exit codes 124, 134, 137, 139 or > 128).  Ordinary test failures (exit 1)
+# do not stop the session.  Usage: tools/gpu_session.sh STEP...   (steps: test smoke bench prof pmc)
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/session.log
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 )) s)" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name: stopping" | tee -a gpurun_out/session.log; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    test)  run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q -s ;;
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
