@@ -20,6 +20,7 @@
 #include "rrt_internal.h"
 
 hipError_t rrt_launch_render(const KParams& kp, int deep, int count, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -82,6 +83,7 @@ struct rrt_ctx {
   std::vector<BNode> nodes;
   std::vector<uint32_t> leaf;
   uint32_t max_depth = 0;
+  bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (rrt_mega.hip)
   std::vector<DBsdf> bsdfs;
   std::vector<DLight> lights;
   bool has_scene = false, has_camera = false;
@@ -302,6 +304,16 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
       c->nodes[n.right].skip = n.skip;
     }
   }
+  // Markstein-corrected slab quotients are exact when no quotient or residual can
+  // under/overflow: require every BVH coordinate to be 0 or of magnitude in [2^-800, 2^20]
+  c->fast_div = true;
+  for (const BNode& n : c->nodes) {
+    const double v[6] = {n.bb.mn.x, n.bb.mn.y, n.bb.mn.z, n.bb.mx.x, n.bb.mx.y, n.bb.mx.z};
+    for (double x : v) {
+      double a = std::fabs(x);
+      if (!(x == 0.0 || (a >= 0x1p-800 && a <= 0x1p20))) c->fast_div = false;
+    }
+  }
   // device layout
   std::vector<DNode> dn(c->nodes.size());
   for (size_t i = 0; i < c->nodes.size(); ++i) {
@@ -424,6 +436,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   KParams kp{};
   kp.nodes = c->d_nodes; kp.geo = c->d_geo; kp.nrm = c->d_nrm; kp.meta = c->d_meta;
   kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size();
+  kp.fast_div = (c->fast_div && !(p->flags & RRT_RENDER_EXACT_DIV)) ? 1u : 0u;
   kp.cam = c->cam; kp.hole = c->hole;
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
@@ -439,13 +452,19 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // persistent grid: 4 waves per block, at most 4 blocks per CU resident, never more blocks
   // than there are 8x8 pixel blocks to pull
   uint32_t want = (kp.n_blocks + 3) / 4;
-  uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 4u);
+  const bool mega = !(p->max_ray_depth >= 2) && !(p->flags & RRT_RENDER_GENERAL);
+  const int waves = (p->variant >= 1 && p->variant <= 4) ? (int)p->variant : 2;
+  const uint32_t per_cu = mega ? (uint32_t)waves : 4u;
+  uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * per_cu);
   if (grid == 0) grid = 1;
   c->last_grid = grid;
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
   HIPCHK(c, hipEventRecord(c->ev0, stream));
-  HIPCHK(c, rrt_launch_render(kp, deep, count, grid, stream));
+  if (mega)
+    HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
+  else
+    HIPCHK(c, rrt_launch_render(kp, deep, count, grid, stream));
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
   return RRT_OK;

@@ -62,7 +62,7 @@ struct KParams {
   const DBsdf* bsdfs;
   const DLight* lights;
   uint32_t n_lights;
-  uint32_t pad0;
+  uint32_t fast_div;  // scene bounds allow the Markstein-corrected slab quotients (rrt_mega.hip)
   DCamera cam;
   DHole hole;
   // render

@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librrt.so")
 
 RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
-RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS = 1, 2
+RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_GENERAL, RRT_RENDER_EXACT_DIV = 1, 2, 4, 8
 
 
 class RRTError(RuntimeError):
@@ -49,7 +49,7 @@ class RenderParams(C.Structure):
     _fields_ = [("ns_aa", C.c_uint32), ("max_ray_depth", C.c_uint32), ("ns_area_light", C.c_uint32),
                 ("samples_per_batch", C.c_uint32), ("max_tolerance", C.c_float),
                 ("direct_hemisphere", C.c_uint32), ("seed", C.c_uint64), ("frame_w", C.c_uint32),
-                ("frame_h", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+                ("frame_h", C.c_uint32), ("flags", C.c_uint32), ("variant", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -133,12 +133,12 @@ def load_camera(path):
 
 
 def render_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
-                  max_tolerance=0.05, direct_hemisphere=False, seed=0, flags=0):
+                  max_tolerance=0.05, direct_hemisphere=False, seed=0, flags=0, variant=0):
     p = RenderParams()
     lib().rrt_render_params_default(C.byref(p))
     p.ns_aa, p.max_ray_depth, p.ns_area_light = ns_aa, max_ray_depth, ns_area_light
     p.samples_per_batch, p.max_tolerance, p.direct_hemisphere = samples_per_batch, max_tolerance, int(direct_hemisphere)
-    p.seed, p.frame_w, p.frame_h, p.flags = seed, frame_w, frame_h, flags
+    p.seed, p.frame_w, p.frame_h, p.flags, p.variant = seed, frame_w, frame_h, flags, variant
     return p
 
 

@@ -24,6 +24,7 @@ for step in "$@"; do
     bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    ab)    run ab 900 python3 tools/ab_kernels.py --rounds 3 ${AB_VARIANTS:-general:4:0 mega1:0:1 mega2:0:2 mega3:0:3 mega4:0:4 mega2x:8:2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
