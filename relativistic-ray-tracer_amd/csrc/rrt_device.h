@@ -89,14 +89,42 @@ __device__ __forceinline__ v3 hemisphere_sample(Rng& g) {  // sampler.cpp:15-29 
 struct Counters { uint32_t bbox, micro, prim, query; };
 
 // ------------------------------------------------------------------ geometry
-// BBox::intersect (bbox.cpp:10-25); min_t is 0 for every micro segment
-__device__ __forceinline__ bool bbox_hit(const DNode& n, v3 o, v3 d, double max_t) {
-  double tx0 = (n.mn[0] - o.x) / d.x, tx1 = (n.mx[0] - o.x) / d.x,
-         ty0 = (n.mn[1] - o.y) / d.y, ty1 = (n.mx[1] - o.y) / d.y,
-         tz0 = (n.mn[2] - o.z) / d.z, tz1 = (n.mx[2] - o.z) / d.z,
-         tmin = std_max(std_max(std_min(tx0, tx1), std_min(ty0, ty1)), std_min(tz0, tz1)),
+// Correctly rounded a / b given y = RN(1/b): two Markstein correction steps (residuals exact by
+// FMA).  Equals IEEE a / b whenever nothing under/overflows (Markstein's theorem); callers only
+// use it in ranges where that is guaranteed (see in_fast_range / rrt_host.cpp fast_div).
+__device__ __forceinline__ double qdiv(double a, double b, double y) {
+  double q0 = a * y;
+  double r0 = fma(-q0, b, a);
+  double q1 = fma(r0, y, q0);
+  double r1 = fma(-q1, b, a);
+  return fma(r1, y, q1);
+}
+__device__ __forceinline__ bool in_fast_range(double v) {
+  const double a = fabs(v);
+  return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
+}
+// BBox::intersect (bbox.cpp:10-25), dividing by the segment direction; min_t is 0 for every
+// micro segment.  EXACT: IEEE division; else qdiv with the per-segment reciprocals y.
+template <bool EXACT>
+__device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double max_t) {
+  double tx0, tx1, ty0, ty1, tz0, tz1;
+  if (EXACT) {
+    tx0 = (n.mn[0] - o.x) / d.x; tx1 = (n.mx[0] - o.x) / d.x;
+    ty0 = (n.mn[1] - o.y) / d.y; ty1 = (n.mx[1] - o.y) / d.y;
+    tz0 = (n.mn[2] - o.z) / d.z; tz1 = (n.mx[2] - o.z) / d.z;
+  } else {
+    tx0 = qdiv(n.mn[0] - o.x, d.x, y.x); tx1 = qdiv(n.mx[0] - o.x, d.x, y.x);
+    ty0 = qdiv(n.mn[1] - o.y, d.y, y.y); ty1 = qdiv(n.mx[1] - o.y, d.y, y.y);
+    tz0 = qdiv(n.mn[2] - o.z, d.z, y.z); tz1 = qdiv(n.mx[2] - o.z, d.z, y.z);
+  }
+  double tmin = std_max(std_max(std_min(tx0, tx1), std_min(ty0, ty1)), std_min(tz0, tz1)),
          tmax = std_min(std_min(std_max(tx0, tx1), std_max(ty0, ty1)), std_max(tz0, tz1));
   return tmin <= tmax && tmin <= max_t && tmax >= 0.0;
+}
+// May the segment (o, d) use qdiv?  Quotients (n - o) / d then stay in [2^-852, 2^820] or 0.
+__device__ __forceinline__ bool segment_fast(const KParams& kp, v3 o, v3 d) {
+  return kp.fast_div && in_fast_range(o.x) && in_fast_range(o.y) && in_fast_range(o.z) &&
+         fabs(d.x) >= 0x1p-800 && fabs(d.y) >= 0x1p-800 && fabs(d.z) >= 0x1p-800;
 }
 // Sphere::test + the range checks of Sphere::intersect (sphere.cpp:10-53), min_t = 0
 __device__ __forceinline__ bool sphere_t(v3 c, double r2, v3 o, v3 d, double max_t, double& t) {
@@ -123,15 +151,15 @@ struct Isect { v3 hit_p, w_out, n; int bsdf; };
 
 // BVHAccel::intersect_micro (bvh.cpp:115-138) for one micro segment.  ANY: shadow query, stop
 // at the first accepted primitive (only the boolean is used; result-identical).
-template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool traverse(const KParams& kp, v3 o, v3 d, double& max_t, int& hit_slot,
+template <bool ANY, bool COUNT, bool EXACT>
+__device__ __forceinline__ bool traverse(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
                                          double& hb1, double& hb2, Counters& cn) {
   bool hit = false;
   int node = 0;
   while (node >= 0) {
     const DNode n = kp.nodes[node];
     if (COUNT) cn.bbox++;
-    if (!bbox_hit(n, o, d, max_t)) { node = n.skip; continue; }
+    if (!slab<EXACT>(n, o, d, y, max_t)) { node = n.skip; continue; }
     if (n.count == 0) { node = node + 1; continue; }
     for (int i = 0; i < n.count; ++i) {
       const int slot = n.first + i;
@@ -193,7 +221,10 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
     if (sphere_t(hc, kp.hole.r2, o, d, max_t, tc)) return false;  // captured
     int slot = -1;
     double b1 = 0, b2 = 0, seg_t = max_t;
-    if (traverse<ANY, COUNT>(kp, o, d, seg_t, slot, b1, b2, cn)) {
+    const v3 y = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const bool hit = segment_fast(kp, o, d) ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
+                                            : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
+    if (hit) {
       if (!ANY) {
         const DPrimMeta meta = kp.meta[slot];
         is->bsdf = (int)((meta >> 8) & 0xffu);

@@ -19,7 +19,7 @@
 #include "../../include/rrt_scene_format.h"
 #include "rrt_internal.h"
 
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
@@ -464,7 +464,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (mega)
     HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
   else
-    HIPCHK(c, rrt_launch_render(kp, deep, count, grid, stream));
+    HIPCHK(c, rrt_launch_render(kp, deep, count, waves, grid, stream));
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
   return RRT_OK;

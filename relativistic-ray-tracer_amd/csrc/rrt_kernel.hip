@@ -147,8 +147,8 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
 }  // namespace rrt
 
 // ------------------------------------------------------------------ kernels
-template <bool DEEP, bool COUNT>
-__global__ __launch_bounds__(256) void rrt_render_kernel(KParams kp) {
+template <bool DEEP, bool COUNT, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(KParams kp) {
   using namespace rrt;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t bpt = kp.blocks_per_tile_side;
@@ -212,11 +212,13 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
 }
 
 // ------------------------------------------------------------------ launch shims (C++ linkage)
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, uint32_t grid, hipStream_t stream) {
-  if (deep && count) hipLaunchKernelGGL((rrt_render_kernel<true, true>), dim3(grid), dim3(256), 0, stream, kp);
-  else if (deep) hipLaunchKernelGGL((rrt_render_kernel<true, false>), dim3(grid), dim3(256), 0, stream, kp);
-  else if (count) hipLaunchKernelGGL((rrt_render_kernel<false, true>), dim3(grid), dim3(256), 0, stream, kp);
-  else hipLaunchKernelGGL((rrt_render_kernel<false, false>), dim3(grid), dim3(256), 0, stream, kp);
+// waves: register budget (minimum waves per SIMD) of the fast depth<=1 variant, A/B knob
+hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int waves, uint32_t grid, hipStream_t stream) {
+  if (deep && count) hipLaunchKernelGGL((rrt_render_kernel<true, true, 1>), dim3(grid), dim3(256), 0, stream, kp);
+  else if (deep) hipLaunchKernelGGL((rrt_render_kernel<true, false, 1>), dim3(grid), dim3(256), 0, stream, kp);
+  else if (count) hipLaunchKernelGGL((rrt_render_kernel<false, true, 1>), dim3(grid), dim3(256), 0, stream, kp);
+  else if (waves >= 2) hipLaunchKernelGGL((rrt_render_kernel<false, false, 2>), dim3(grid), dim3(256), 0, stream, kp);
+  else hipLaunchKernelGGL((rrt_render_kernel<false, false, 1>), dim3(grid), dim3(256), 0, stream, kp);
   return hipGetLastError();
 }
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,

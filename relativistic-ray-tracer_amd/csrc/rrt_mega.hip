@@ -25,36 +25,6 @@
 
 namespace rrt {
 
-__device__ __forceinline__ double qdiv(double a, double b, double y) {
-  double q0 = a * y;
-  double r0 = fma(-q0, b, a);
-  double q1 = fma(r0, y, q0);
-  double r1 = fma(-q1, b, a);
-  return fma(r1, y, q1);
-}
-
-template <bool EXACT>
-__device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double max_t) {
-  double tx0, tx1, ty0, ty1, tz0, tz1;
-  if (EXACT) {
-    tx0 = (n.mn[0] - o.x) / d.x; tx1 = (n.mx[0] - o.x) / d.x;
-    ty0 = (n.mn[1] - o.y) / d.y; ty1 = (n.mx[1] - o.y) / d.y;
-    tz0 = (n.mn[2] - o.z) / d.z; tz1 = (n.mx[2] - o.z) / d.z;
-  } else {
-    tx0 = qdiv(n.mn[0] - o.x, d.x, y.x); tx1 = qdiv(n.mx[0] - o.x, d.x, y.x);
-    ty0 = qdiv(n.mn[1] - o.y, d.y, y.y); ty1 = qdiv(n.mx[1] - o.y, d.y, y.y);
-    tz0 = qdiv(n.mn[2] - o.z, d.z, y.z); tz1 = qdiv(n.mx[2] - o.z, d.z, y.z);
-  }
-  double tmin = std_max(std_max(std_min(tx0, tx1), std_min(ty0, ty1)), std_min(tz0, tz1)),
-         tmax = std_min(std_min(std_max(tx0, tx1), std_max(ty0, ty1)), std_max(tz0, tz1));
-  return tmin <= tmax && tmin <= max_t && tmax >= 0.0;
-}
-
-__device__ __forceinline__ bool in_fast_range(double v) {
-  const double a = fabs(v);
-  return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
-}
-
 // BVHAccel::intersect_micro (bvh.cpp:115-138) over one micro segment, stackless (skip pointers)
 template <bool EXACT, bool COUNT>
 __device__ __forceinline__ bool seg_traverse(const KParams& kp, v3 o, v3 d, v3 y, double max_t, bool any,
@@ -197,8 +167,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(KParams kp) {
         done = true;  // captured by the hole: "no hit" (bvh.cpp:107-108)
       } else {
         const v3 y = V(1.0 / qd.x, 1.0 / qd.y, 1.0 / qd.z);
-        const bool fast = kp.fast_div && in_fast_range(qo.x) && in_fast_range(qo.y) && in_fast_range(qo.z) &&
-                          fabs(qd.x) >= 0x1p-800 && fabs(qd.y) >= 0x1p-800 && fabs(qd.z) >= 0x1p-800;
+        const bool fast = segment_fast(kp, qo, qd);
         const bool any = (qkind == Q_SHADOW);
         if (fast) qhit = seg_traverse<false, COUNT>(kp, qo, qd, y, qmax, any, qslot, qt, qb1, qb2, cn);
         else qhit = seg_traverse<true, COUNT>(kp, qo, qd, y, qmax, any, qslot, qt, qb1, qb2, cn);
