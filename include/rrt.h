@@ -131,8 +131,8 @@ typedef struct {
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
   RRT_RENDER_DRAWS = 1u << 1,    /* also produce per-pixel RNG draw counts */
-  RRT_RENDER_GENERAL = 1u << 2,  /* force the general (any depth) kernel instead of the
-                                    depth <= 1 wavefront state machine (A/B testing) */
+  RRT_RENDER_WAVEFRONT = 1u << 2, /* depth <= 1: use the wavefront state-machine kernel
+                                     instead of the general kernel (A/B testing) */
   RRT_RENDER_EXACT_DIV = 1u << 3 /* slab tests by true division instead of the
                                     Markstein-corrected reciprocal (A/B testing) */
 };

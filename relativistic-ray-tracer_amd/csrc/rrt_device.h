@@ -297,9 +297,11 @@ __device__ __forceinline__ spec mf_f(const DBsdf& b, v3 wo, v3 wi) {
   double D = mf_D(alpha, unit(wo + wi));
   return ((mf_F(b, wi) * (float)G) * (float)D) / (float)(4 * wo.z * wi.z);
 }
+// LEAN: the scene has no microfacet BSDF (only diffuse / emission / delta BSDFs reach f)
+template <bool LEAN = false>
 __device__ __forceinline__ spec bsdf_f(const DBsdf& b, v3 wo, v3 wi) {
   if (b.type == B_DIFFUSE) return S(b.p[0], b.p[1], b.p[2]) / (float)PI_D;
-  if (b.type == B_MICROFACET) return mf_f(b, wo, wi);
+  if (!LEAN && b.type == B_MICROFACET) return mf_f(b, wo, wi);
   return S(0, 0, 0);
 }
 __device__ __forceinline__ bool refract(v3 wo, v3& wi, float ior) {  // bsdf.cpp:146-159
@@ -365,9 +367,11 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf)
 }
 
 // ------------------------------------------------------------------ lights (light.cpp)
+// LEAN: every light is an area light
+template <bool LEAN = false>
 __device__ spec light_sample_L(const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
-  switch (l.type) {
+  switch (LEAN ? 0u : l.type) {
     case 0: {  // AreaLight::sample_L (light.cpp:80-92): float sqDist, sqrtf, float pdf
       double sx, sy;
       g.grid(sx, sy);

@@ -19,7 +19,8 @@
 #include "../../include/rrt_scene_format.h"
 #include "rrt_internal.h"
 
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, int waves, uint32_t grid,
+                             hipStream_t stream);
 hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
@@ -83,7 +84,8 @@ struct rrt_ctx {
   std::vector<BNode> nodes;
   std::vector<uint32_t> leaf;
   uint32_t max_depth = 0;
-  bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (rrt_mega.hip)
+  bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (qdiv, rrt_device.h)
+  bool lean = false;      // area lights only and no microfacet BSDF (LEAN kernel builds)
   std::vector<DBsdf> bsdfs;
   std::vector<DLight> lights;
   bool has_scene = false, has_camera = false;
@@ -345,6 +347,9 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
       meta[k] = (p.bsdf << 8) | 1u;
     }
   }
+  c->lean = true;
+  for (const DLight& l : c->lights) if (l.type != RRT_LIGHT_AREA) c->lean = false;
+  for (const DBsdf& b : c->bsdfs) if (b.type == RRT_BSDF_MICROFACET) c->lean = false;
   c->has_scene = true;
   if (c->device < 0) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -449,22 +454,26 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.block_counter = c->d_counter;
   kp.clip_x0 = cx0; kp.clip_y0 = cy0; kp.clip_x1 = cx1; kp.clip_y1 = cy1;
   kp.rgb = d_rgb; kp.count = d_cnt; kp.draws = d_draws; kp.counters = d_ctr;
-  // persistent grid: 4 waves per block, at most 4 blocks per CU resident, never more blocks
-  // than there are 8x8 pixel blocks to pull
-  uint32_t want = (kp.n_blocks + 3) / 4;
-  const bool mega = !(p->max_ray_depth >= 2) && !(p->flags & RRT_RENDER_GENERAL);
-  const int waves = (p->variant >= 1 && p->variant <= 4) ? (int)p->variant : 2;
-  const uint32_t per_cu = mega ? (uint32_t)waves : 4u;
-  uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * per_cu);
-  if (grid == 0) grid = 1;
-  c->last_grid = grid;
+  // Kernel choice.  Default: the general kernel (one lane = one pixel, the reference's loops),
+  // LEAN build when the scene allows it.  RRT_RENDER_WAVEFRONT selects the state-machine kernel
+  // (rrt_mega.hip, depth <= 1).  variant = register budget in waves per SIMD (default 2).
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
+  const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
+  const int lean = (!deep && !count && c->lean && !p->direct_hemisphere) ? 1 : 0;
+  const int waves = (p->variant >= 1 && p->variant <= 4) ? (int)p->variant : 2;
+  // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
+  // blocks as the kernel's registers allow become resident; any others start when a resident
+  // block exits and find the atomic work counter exhausted
+  uint32_t want = (kp.n_blocks + 3) / 4;
+  uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
+  if (grid == 0) grid = 1;
+  c->last_grid = grid;
   HIPCHK(c, hipEventRecord(c->ev0, stream));
   if (mega)
     HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
   else
-    HIPCHK(c, rrt_launch_render(kp, deep, count, waves, grid, stream));
+    HIPCHK(c, rrt_launch_render(kp, deep, count, lean, waves, grid, stream));
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
   return RRT_OK;

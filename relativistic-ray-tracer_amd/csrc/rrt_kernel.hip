@@ -12,10 +12,11 @@
 namespace rrt {
 
 // ------------------------------------------------------------------ integrator (part1_code.cpp)
-template <bool COUNT>
+// LEAN: area lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
+// (same values: make_coord_space is a pure function of the normal) instead of being kept live
+// across the shadow query, which keeps 12 VGPRs out of the traversal loop.
+template <bool COUNT, bool LEAN>
 __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :33-57
-  Frame f = coord_space(is.n);
-  v3 w_out = to_local(f, is.w_out);
   const DBsdf b = kp.bsdfs[is.bsdf];
   spec L = S(0, 0, 0);
   int total = 0;
@@ -25,11 +26,12 @@ __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Co
     total += num;
     for (int i = 0; i < num; ++i) {
       v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L(l, g, is.hit_p, wi_world, dist, pdf);
+      spec sample = light_sample_L<LEAN>(l, g, is.hit_p, wi_world, dist, pdf);
+      const Frame f = coord_space(is.n);
       v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
-      if (!query<true, COUNT>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn))
-        L = L + ((sample * bsdf_f(b, w_out, w_in)) * (float)w_in.z) / pdf;
+      spec contrib = ((sample * bsdf_f<LEAN>(b, to_local(f, is.w_out), w_in)) * (float)w_in.z) / pdf;
+      if (!query<true, COUNT>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
     }
   }
   return L / (float)total;
@@ -52,9 +54,10 @@ __device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Co
   return ((L * 2.0f) * (float)PI_D) / (float)num;
 }
 
-template <bool COUNT>
+template <bool COUNT, bool LEAN = false>
 __device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {
-  return kp.direct_hemisphere ? direct_hemisphere<COUNT>(kp, g, is, cn) : direct_importance<COUNT>(kp, g, is, cn);
+  if (LEAN) return direct_importance<COUNT, true>(kp, g, is, cn);
+  return kp.direct_hemisphere ? direct_hemisphere<COUNT>(kp, g, is, cn) : direct_importance<COUNT, false>(kp, g, is, cn);
 }
 
 // at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
@@ -105,18 +108,18 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
   return L;
 }
 
-template <bool DEEP, bool COUNT>
+template <bool DEEP, bool COUNT, bool LEAN>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
   if (!query<false, COUNT>(kp, o, d, &is, cn)) return S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
-  if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT>(kp, g, is, cn);
+  if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN>(kp, g, is, cn);
   return e + at_least_one_bounce<COUNT>(kp, g, is, cn);
 }
 
 // PathTracer::raytrace_pixel (:125-163) with ADAPTIVE == 1, THIN_LENS == 0
-template <bool DEEP, bool COUNT>
+template <bool DEEP, bool COUNT, bool LEAN>
 __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
   spec ret = S(0, 0, 0);
   int i;
@@ -130,7 +133,7 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
     double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
     double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
-    spec s = est_radiance<DEEP, COUNT>(kp, g, ld3(cam.pos), unit(w), cn);
+    spec s = est_radiance<DEEP, COUNT, LEAN>(kp, g, ld3(cam.pos), unit(w), cn);
     ret = ret + s;
     double il = illum(s);
     s1 += il;
@@ -147,7 +150,10 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
 }  // namespace rrt
 
 // ------------------------------------------------------------------ kernels
-template <bool DEEP, bool COUNT, int WAVES>
+// DEEP: max_ray_depth >= 2 (bounce loop); COUNT: per-pixel work counters; LEAN: area lights
+// only, no microfacet BSDF, importance-sampled direct light (the BASELINE scenes); WAVES: the
+// register budget, as minimum waves per SIMD.
+template <bool DEEP, bool COUNT, bool LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(KParams kp) {
   using namespace rrt;
   const uint32_t lane = threadIdx.x & 63u;
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(KParams kp) {
       Rng g; g.key = rrt_pixel_key(kp.seed, x, y); g.ctr = 0;
       Counters cn = {0, 0, 0, 0};
       int cnt;
-      spec s = raytrace_pixel<DEEP, COUNT>(kp, x, y, cnt, g, cn);
+      spec s = raytrace_pixel<DEEP, COUNT, LEAN>(kp, x, y, cnt, g, cn);
       const size_t k = (size_t)t * tpix + (size_t)ly * kp.tile_size + lx;
       kp.rgb[3 * k] = s.r; kp.rgb[3 * k + 1] = s.g; kp.rgb[3 * k + 2] = s.b;
       kp.count[k] = cnt;
@@ -212,13 +218,26 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
 }
 
 // ------------------------------------------------------------------ launch shims (C++ linkage)
-// waves: register budget (minimum waves per SIMD) of the fast depth<=1 variant, A/B knob
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int waves, uint32_t grid, hipStream_t stream) {
-  if (deep && count) hipLaunchKernelGGL((rrt_render_kernel<true, true, 1>), dim3(grid), dim3(256), 0, stream, kp);
-  else if (deep) hipLaunchKernelGGL((rrt_render_kernel<true, false, 1>), dim3(grid), dim3(256), 0, stream, kp);
-  else if (count) hipLaunchKernelGGL((rrt_render_kernel<false, true, 1>), dim3(grid), dim3(256), 0, stream, kp);
-  else if (waves >= 2) hipLaunchKernelGGL((rrt_render_kernel<false, false, 2>), dim3(grid), dim3(256), 0, stream, kp);
-  else hipLaunchKernelGGL((rrt_render_kernel<false, false, 1>), dim3(grid), dim3(256), 0, stream, kp);
+// Kernel selection: deep / counting variants are built once (1 wave per SIMD budget); the
+// depth <= 1 path has general and LEAN builds at 1..4 waves per SIMD (A/B knob `waves`).
+hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, int waves, uint32_t grid,
+                             hipStream_t stream) {
+#define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, kp)
+  if (deep) {
+    if (count) RRT_LAUNCH(true, true, false, 1); else RRT_LAUNCH(true, false, false, 1);
+  } else if (count) {
+    RRT_LAUNCH(false, true, false, 1);
+  } else if (lean) {
+    switch (waves) {
+      case 1: RRT_LAUNCH(false, false, true, 1); break;
+      case 3: RRT_LAUNCH(false, false, true, 3); break;
+      case 4: RRT_LAUNCH(false, false, true, 4); break;
+      default: RRT_LAUNCH(false, false, true, 2); break;
+    }
+  } else {
+    if (waves == 1) RRT_LAUNCH(false, false, false, 1); else RRT_LAUNCH(false, false, false, 2);
+  }
+#undef RRT_LAUNCH
   return hipGetLastError();
 }
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,

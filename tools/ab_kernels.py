@@ -4,7 +4,7 @@
 Renders a golden workload with each variant, checks it against the reference's golden frame
 (bit-exact), and reports the HIP-event kernel time per variant (median / min over rounds).
 Usage: python3 tools/ab_kernels.py [--case cfg3_bunny_1080p_s64] [--rounds 3] VARIANT...
-VARIANT = name:flags:variant, e.g. general:4:0  mega2:0:2  mega2x:8:2
+VARIANT = name:flags:variant, e.g. lean2:0:2  mega2:4:2  lean2x:8:2 (flags: rrt.h RRT_RENDER_*)
 """
 import argparse
 import json

@@ -23,11 +23,11 @@ for step in "$@"; do
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-general:4:0 mega2:0:2}
-           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-general:4:0 mega2:0:2}
-           run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-general:4:0 mega2:0:2}
-           run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-general:4:0 mega2:0:2} ;;
-    ab)    run ab 900 python3 tools/ab_kernels.py --rounds 3 ${AB_VARIANTS:-general:4:0 mega1:0:1 mega2:0:2 mega3:0:3 mega4:0:4 mega2x:8:2} ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
+           run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
+           run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2} ;;
+    ab)    run ab 900 python3 tools/ab_kernels.py --rounds 3 ${AB_VARIANTS:-lean1:0:1 lean2:0:2 lean3:0:3 lean4:0:4 mega2:4:2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
