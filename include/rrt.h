@@ -125,16 +125,17 @@ typedef struct {
   uint64_t seed;              /* keyed RNG seed */
   uint32_t frame_w, frame_h;  /* sampleBuffer.w / h (set_frame_size) */
   uint32_t flags;             /* RRT_RENDER_* */
-  uint32_t variant;           /* 0 = default; 1..4 = waves/SIMD the depth<=1 kernel is built
+  uint32_t variant;           /* 0 = default; 1..5 = waves/SIMD the depth<=1 kernel is built
                                  for (register budget), for A/B measurements */
 } rrt_render_params;
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
   RRT_RENDER_DRAWS = 1u << 1,    /* also produce per-pixel RNG draw counts */
-  RRT_RENDER_WAVEFRONT = 1u << 2, /* depth <= 1: use the wavefront state-machine kernel
-                                     instead of the general kernel (A/B testing) */
-  RRT_RENDER_EXACT_DIV = 1u << 3 /* slab tests by true division instead of the
-                                    Markstein-corrected reciprocal (A/B testing) */
+  RRT_RENDER_WAVEFRONT = 1u << 2, /* depth <= 1: wavefront state-machine kernel (A/B testing) */
+  RRT_RENDER_EXACT_DIV = 1u << 3, /* slab tests by true division instead of the
+                                     Markstein-corrected reciprocal (A/B testing) */
+  RRT_RENDER_PIXEL_LOOP = 1u << 4 /* depth <= 1: per-pixel-loop kernel instead of the default
+                                     per-sample kernel (A/B testing) */
 };
 void rrt_render_params_default(rrt_render_params* p);
 

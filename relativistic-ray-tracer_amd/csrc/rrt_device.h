@@ -116,6 +116,12 @@ __device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double ma
     tx0 = qdiv(n.mn[0] - o.x, d.x, y.x); tx1 = qdiv(n.mx[0] - o.x, d.x, y.x);
     ty0 = qdiv(n.mn[1] - o.y, d.y, y.y); ty1 = qdiv(n.mx[1] - o.y, d.y, y.y);
     tz0 = qdiv(n.mn[2] - o.z, d.z, y.z); tz1 = qdiv(n.mx[2] - o.z, d.z, y.z);
+    // On a fast segment every quotient is finite (|d| >= 2^-800, |n - o| <= 2^21), so
+    // std::min/max (NaN -> first argument) and the hardware v_min/max_f64 agree except on the
+    // sign of a zero, which no comparison below can see.
+    const double tmin = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmin(tz0, tz1)),
+                 tmax = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmax(tz0, tz1));
+    return tmin <= tmax && tmin <= max_t && tmax >= 0.0;
   }
   double tmin = std_max(std_max(std_min(tx0, tx1), std_min(ty0, ty1)), std_min(tz0, tz1)),
          tmax = std_min(std_min(std_max(tx0, tx1), std_max(ty0, ty1)), std_max(tz0, tz1));

@@ -22,6 +22,7 @@
 hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream);
 hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_sample(const KParams& kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -454,14 +455,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.block_counter = c->d_counter;
   kp.clip_x0 = cx0; kp.clip_y0 = cy0; kp.clip_x1 = cx1; kp.clip_y1 = cy1;
   kp.rgb = d_rgb; kp.count = d_cnt; kp.draws = d_draws; kp.counters = d_ctr;
-  // Kernel choice.  Default: the general kernel (one lane = one pixel, the reference's loops),
-  // LEAN build when the scene allows it.  RRT_RENDER_WAVEFRONT selects the state-machine kernel
-  // (rrt_mega.hip, depth <= 1).  variant = register budget in waves per SIMD (default 2).
+  // Kernel choice (depth <= 1): the per-sample kernel (rrt_sample.hip) by default;
+  // RRT_RENDER_PIXEL_LOOP selects the general per-pixel-loop kernel (rrt_kernel.hip, also used
+  // for depth >= 2) and RRT_RENDER_WAVEFRONT the state-machine kernel (rrt_mega.hip).  LEAN
+  // builds when the scene allows them; variant = register budget in waves per SIMD.
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
   const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
+  const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
   const int lean = (!deep && !count && c->lean && !p->direct_hemisphere) ? 1 : 0;
-  const int waves = (p->variant >= 1 && p->variant <= 4) ? (int)p->variant : 2;
+  const int waves = (p->variant >= 1 && p->variant <= 5) ? (int)p->variant : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
@@ -472,8 +475,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   HIPCHK(c, hipEventRecord(c->ev0, stream));
   if (mega)
     HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
-  else
+  else if (pixel_loop)
     HIPCHK(c, rrt_launch_render(kp, deep, count, lean, waves, grid, stream));
+  else
+    HIPCHK(c, rrt_launch_sample(kp, count, lean, waves, grid, stream));
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
   return RRT_OK;

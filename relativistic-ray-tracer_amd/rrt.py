@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, "librrt.so")
 
 RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
 RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DIV = 1, 2, 4, 8
+RRT_RENDER_PIXEL_LOOP = 16
 
 
 class RRTError(RuntimeError):
