@@ -34,14 +34,56 @@ __device__ __forceinline__ double dot(v3 u, v3 v) { return u.x * v.x + u.y * v.y
 __device__ __forceinline__ v3 cross(v3 u, v3 v) {
   return V(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
-__device__ __forceinline__ double norm(v3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+// Correctly rounded f64 sqrt / division, in-range fast path.  hipcc lowers sqrt and `/` to
+// range-scaling wrappers (v_cmp + v_ldexp / v_div_scale, v_div_fmas, v_div_fixup, class
+// checks) around a core of v_rsq / v_rcp + FMA refinements.  For operands of magnitude in
+// [2^-300, 2^300] the scaling is never triggered and the fix-ups are identities, so the bare
+// core below returns the same bits (checked bit for bit by tests/test_gpu_parity.py); other
+// operands take the library path.  RRT_LIBM_DIVSQRT=1 builds without the fast path (A/B).
+#ifndef RRT_LIBM_DIVSQRT
+#define RRT_LIBM_DIVSQRT 0
+#endif
+__device__ __forceinline__ bool in_core_range(double v) {
+  const double a = fabs(v);
+  return a >= 0x1p-300 && a <= 0x1p300;
+}
+__device__ __forceinline__ double sqrt_core(double x) {  // = llvm f64 sqrt expansion, scale 0
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  double d = fma(-g, g, x);
+  h = fma(h, r, h);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+}
+__device__ __forceinline__ double div_core(double a, double b) {  // = llvm f64 fdiv, no scaling
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  const double q = a * y;
+  const double r = fma(-b, q, a);
+  return fma(r, y, q);
+}
+__device__ __forceinline__ double xsqrt(double x) {
+  if (RRT_LIBM_DIVSQRT || __builtin_expect(!in_core_range(x), 0)) return sqrt(x);
+  return sqrt_core(x);
+}
+__device__ __forceinline__ double xdiv(double a, double b) {
+  if (RRT_LIBM_DIVSQRT || __builtin_expect(!(in_core_range(a) && in_core_range(b)), 0)) return a / b;
+  return div_core(a, b);
+}
+__device__ __forceinline__ double norm(v3 a) { return xsqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
 __device__ __forceinline__ double norm2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 __device__ __forceinline__ v3 unit(v3 a) {
-  double r = 1. / sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+  double r = xdiv(1., xsqrt(a.x * a.x + a.y * a.y + a.z * a.z));
   return V(r * a.x, r * a.y, r * a.z);
 }
-__device__ __forceinline__ v3 normalize(v3 a) { double c = 1. / norm(a); return V(a.x * c, a.y * c, a.z * c); }
-__device__ __forceinline__ v3 divd(v3 a, double c) { double rc = 1.0 / c; return V(rc * a.x, rc * a.y, rc * a.z); }
+__device__ __forceinline__ v3 normalize(v3 a) { double c = xdiv(1., norm(a)); return V(a.x * c, a.y * c, a.z * c); }
+__device__ __forceinline__ v3 divd(v3 a, double c) { double rc = xdiv(1.0, c); return V(rc * a.x, rc * a.y, rc * a.z); }
 __device__ __forceinline__ double std_min(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
 __device__ __forceinline__ v3 ld3(const double* p) { return V(p[0], p[1], p[2]); }
@@ -147,7 +189,7 @@ __device__ __forceinline__ bool tri_t(const DPrimGeo& gp, v3 o, v3 d, double max
                                       double& b2o) {
   v3 p0 = V(gp.v[0], gp.v[1], gp.v[2]), e1 = V(gp.v[3], gp.v[4], gp.v[5]), e2 = V(gp.v[6], gp.v[7], gp.v[8]);
   v3 s = o - p0, s1 = cross(d, e2), s2 = cross(s, e1);
-  double inv = 1. / dot(s1, e1);
+  double inv = xdiv(1., dot(s1, e1));
   double tt = dot(s2, e2) * inv, b1 = dot(s1, s) * inv, b2 = dot(s2, d) * inv, b0 = 1 - b1 - b2;
   if (0.0 <= tt && tt <= max_t && b0 >= 0 && b1 >= 0 && b2 >= 0) { t = tt; b1o = b1; b2o = b2; return true; }
   return false;
@@ -191,12 +233,12 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
   v3 x_axis = no - V(h.c[0], h.c[1], h.c[2]);
   double dist = norm(x_axis);
   x_axis = normalize(x_axis);
-  double u = 1 / dist;
+  double u = xdiv(1, dist);
   double dx = dot(d, x_axis);
   v3 y_axis = d - smul(dx, x_axis);
   double dy = norm(y_axis);
   y_axis = normalize(y_axis);
-  double up = -u * dx / dy;
+  double up = xdiv(-u * dx, dy);
   const double dt = h.dt, k = 3.0 * h.r;
   double f1 = -u + k * u * u / 2.0;
   double u2 = u + up * dt / 2.0;
@@ -204,7 +246,7 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
   double u3 = u + up * dt / 2.0 + f1 * dt * dt / 4.0;
   double f3 = -u3 + k * u3 * u3 / 2.0;
   u += up * dt + (f1 + f2 + f3) * dt * dt / 6.0;
-  double dd = 1 / u;
+  double dd = xdiv(1, u);
   double next_x = dd * h.cos_dt, next_y = dd * h.sin_dt;
   v3 nd = ((V(h.c[0], h.c[1], h.c[2]) + smul(next_x, x_axis)) + smul(next_y, y_axis)) - no;
   max_t = norm(nd);
@@ -227,7 +269,7 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
     if (sphere_t(hc, kp.hole.r2, o, d, max_t, tc)) return false;  // captured
     int slot = -1;
     double b1 = 0, b2 = 0, seg_t = max_t;
-    const v3 y = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const v3 y = V(xdiv(1.0, d.x), xdiv(1.0, d.y), xdiv(1.0, d.z));
     const bool hit = segment_fast(kp, o, d) ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                                             : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
     if (hit) {

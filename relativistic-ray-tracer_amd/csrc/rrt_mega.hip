@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(KParams kp) {
       if (sphere_t(hc, kp.hole.r2, qo, qd, qmax, tc)) {
         done = true;  // captured by the hole: "no hit" (bvh.cpp:107-108)
       } else {
-        const v3 y = V(1.0 / qd.x, 1.0 / qd.y, 1.0 / qd.z);
+        const v3 y = V(xdiv(1.0, qd.x), xdiv(1.0, qd.y), xdiv(1.0, qd.z));
         const bool fast = segment_fast(kp, qo, qd);
         const bool any = (qkind == Q_SHADOW);
         if (fast) qhit = seg_traverse<false, COUNT>(kp, qo, qd, y, qmax, any, qslot, qt, qb1, qb2, cn);
