@@ -42,7 +42,9 @@ typedef struct rrt_ctx rrt_ctx;
 /* ---------------------------------------------------------------- context */
 typedef struct {
   int device;              /* HIP device ordinal; -1 = host-only context (BVH build, tests) */
-  uint32_t reserved[7];
+  uint32_t free_grid_res;  /* empty-space grid: cells along the root box's longest axis
+                              (0 = default 128, 1 = no grid).  Result-neutral. */
+  uint32_t reserved[6];
 } rrt_device_cfg;
 
 /* Replaces: PathTracer::PathTracer (pathtracer.cpp:32-85) device-side state. */
@@ -134,8 +136,21 @@ enum {
   RRT_RENDER_WAVEFRONT = 1u << 2, /* depth <= 1: wavefront state-machine kernel (A/B testing) */
   RRT_RENDER_EXACT_DIV = 1u << 3, /* slab tests by true division instead of the
                                      Markstein-corrected reciprocal (A/B testing) */
-  RRT_RENDER_PIXEL_LOOP = 1u << 4 /* depth <= 1: per-pixel-loop kernel instead of the default
+  RRT_RENDER_PIXEL_LOOP = 1u << 4, /* depth <= 1: per-pixel-loop kernel instead of the default
                                      per-sample kernel (A/B testing) */
+  RRT_RENDER_NO_SKIP = 1u << 5,   /* traverse every micro segment, ignoring the empty-space
+                                     grid (A/B testing; results are identical) */
+  RRT_RENDER_NO_CLEAN = 1u << 6,  /* walk the reference tree as is, not the clean tree with
+                                     its oversized leaves listed apart (A/B testing; results
+                                     are identical) */
+  RRT_RENDER_PER_PIXEL = 1u << 7, /* depth <= 1: one lane per pixel (per-sample kernel) instead
+                                     of the sample-parallel kernel (A/B testing) */
+  /* diagnostics only -- results are NOT the reference's: */
+  RRT_RENDER_DIAG_NO_INTERIOR = 1u << 28, /* skip walks of segments starting in the root box */
+  RRT_RENDER_DIAG_NO_EXTERIOR = 1u << 29, /* skip walks of segments starting outside it */
+  RRT_RENDER_DIAG_NO_TRAVERSE = 1u << 30, /* skip every BVH traversal (cost of the rest) */
+  RRT_RENDER_DIAG_CLEAR_STATS = 1u << 31  /* with COUNTERS: counter 3 = grid-clear segments,
+                                             counter 2 = AABB tests outside them */
 };
 void rrt_render_params_default(rrt_render_params* p);
 
@@ -176,6 +191,9 @@ int rrt_partition_tiles(uint32_t frame_w, uint32_t frame_h, uint32_t tile_size, 
 typedef struct {
   uint32_t n_prims, n_nodes, n_leaf_refs, max_depth;
   uint64_t device_bytes;      /* HBM held by the scene */
+  uint32_t grid_n[3];         /* empty-space grid cells per axis (0 = none) */
+  uint32_t n_clean, n_big;    /* clean-tree nodes and oversized leaves (0 = reference walk) */
+  float grid_free_frac;       /* fraction of grid cells with free radius > 0 */
   float last_kernel_ms;       /* HIP-event time of the last render launch */
   uint32_t grid_blocks, block_threads;
 } rrt_stats;
@@ -184,6 +202,17 @@ int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
  * right; count 0 = inner node), prims [n_leaf_refs] (build-order primitive ids) -- the layout
  * of the oracle's reference-BVH dump.  Any pointer may be NULL to query sizes via stats. */
 int rrt_get_bvh(const rrt_ctx* ctx, double* boxes, int32_t* nodes, uint32_t* prims);
+
+/* The clean tree the renderer walks: boxes [n][6], nodes [n][4] = (skip, first
+ * slot, slot count (0 = inner), left-first ordinal of the first leaf); oversized leaves:
+ * big_boxes [nb][6], big [nb][3] = (first slot, slot count, ordinal).  Returns n (0 = none);
+ * query nb through rrt_get_stats.  Any pointer may be NULL. */
+int rrt_get_clean_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes, double* big_boxes, int32_t* big);
+
+/* The empty-space grid: k [n[2]][n[1]][n[0]] uint8 Chebyshev cell distances,
+ * geom = {g0.x, g0.y, g0.z, 1/h, h_free}.  Returns the number of cells (0 = no grid); any
+ * pointer may be NULL.  For host-side tests of its conservativeness. */
+int rrt_get_free_grid(const rrt_ctx* ctx, uint8_t* k, double* geom, int32_t* n);
 
 /* ---------------------------------------------------------------- file helpers (.rrts/.rrtc) */
 typedef struct rrt_scene_file rrt_scene_file;

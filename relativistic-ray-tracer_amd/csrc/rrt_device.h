@@ -128,7 +128,22 @@ __device__ __forceinline__ v3 hemisphere_sample(Rng& g) {  // sampler.cpp:15-29 
   return V(xs, ys, zs);
 }
 
-struct Counters { uint32_t bbox, micro, prim, query; };
+#ifndef RRT_PROFILE
+#define RRT_PROFILE 0  // 1: diagnostic build with per-phase cycle counters (tools/phase_profile.py)
+#endif
+struct Counters {
+  uint32_t bbox, micro, prim, query;
+#if RRT_PROFILE
+  uint64_t t_micro, t_trav, t_query;
+#endif
+};
+#if RRT_PROFILE
+#define RRT_T0(v) const uint64_t v = clock64()
+#define RRT_ACC(field, v) cn.field += clock64() - v
+#else
+#define RRT_T0(v)
+#define RRT_ACC(field, v)
+#endif
 
 // ------------------------------------------------------------------ geometry
 // Correctly rounded a / b given y = RN(1/b): two Markstein correction steps (residuals exact by
@@ -148,16 +163,16 @@ __device__ __forceinline__ bool in_fast_range(double v) {
 // BBox::intersect (bbox.cpp:10-25), dividing by the segment direction; min_t is 0 for every
 // micro segment.  EXACT: IEEE division; else qdiv with the per-segment reciprocals y.
 template <bool EXACT>
-__device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double max_t) {
+__device__ __forceinline__ bool slab(const double* mn, const double* mx, v3 o, v3 d, v3 y, double max_t) {
   double tx0, tx1, ty0, ty1, tz0, tz1;
   if (EXACT) {
-    tx0 = (n.mn[0] - o.x) / d.x; tx1 = (n.mx[0] - o.x) / d.x;
-    ty0 = (n.mn[1] - o.y) / d.y; ty1 = (n.mx[1] - o.y) / d.y;
-    tz0 = (n.mn[2] - o.z) / d.z; tz1 = (n.mx[2] - o.z) / d.z;
+    tx0 = (mn[0] - o.x) / d.x; tx1 = (mx[0] - o.x) / d.x;
+    ty0 = (mn[1] - o.y) / d.y; ty1 = (mx[1] - o.y) / d.y;
+    tz0 = (mn[2] - o.z) / d.z; tz1 = (mx[2] - o.z) / d.z;
   } else {
-    tx0 = qdiv(n.mn[0] - o.x, d.x, y.x); tx1 = qdiv(n.mx[0] - o.x, d.x, y.x);
-    ty0 = qdiv(n.mn[1] - o.y, d.y, y.y); ty1 = qdiv(n.mx[1] - o.y, d.y, y.y);
-    tz0 = qdiv(n.mn[2] - o.z, d.z, y.z); tz1 = qdiv(n.mx[2] - o.z, d.z, y.z);
+    tx0 = qdiv(mn[0] - o.x, d.x, y.x); tx1 = qdiv(mx[0] - o.x, d.x, y.x);
+    ty0 = qdiv(mn[1] - o.y, d.y, y.y); ty1 = qdiv(mx[1] - o.y, d.y, y.y);
+    tz0 = qdiv(mn[2] - o.z, d.z, y.z); tz1 = qdiv(mx[2] - o.z, d.z, y.z);
     // On a fast segment every quotient is finite (|d| >= 2^-800, |n - o| <= 2^21), so
     // std::min/max (NaN -> first argument) and the hardware v_min/max_f64 agree except on the
     // sign of a zero, which no comparison below can see.
@@ -169,10 +184,26 @@ __device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double ma
          tmax = std_min(std_min(std_max(tx0, tx1), std_max(ty0, ty1)), std_max(tz0, tz1));
   return tmin <= tmax && tmin <= max_t && tmax >= 0.0;
 }
+template <bool EXACT>
+__device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double max_t) {
+  return slab<EXACT>(n.mn, n.mx, o, d, y, max_t);
+}
 // May the segment (o, d) use qdiv?  Quotients (n - o) / d then stay in [2^-852, 2^820] or 0.
 __device__ __forceinline__ bool segment_fast(const KParams& kp, v3 o, v3 d) {
   return kp.fast_div && in_fast_range(o.x) && in_fast_range(o.y) && in_fast_range(o.z) &&
          fabs(d.x) >= 0x1p-800 && fabs(d.y) >= 0x1p-800 && fabs(d.z) >= 0x1p-800;
+}
+// Is the micro segment [o, o + d max_t] provably clear of every BVH leaf box (DGrid)?  Then the
+// reference's traversal of it tests no primitive and returns "no hit"; skipping it is
+// result-identical.  Points outside the grid answer "not provably clear".
+__device__ __forceinline__ bool segment_clear(const DGrid& g, v3 o, double max_t) {
+  if (!g.k) return false;
+  const double fx = (o.x - g.g0[0]) * g.inv_h, fy = (o.y - g.g0[1]) * g.inv_h, fz = (o.z - g.g0[2]) * g.inv_h;
+  if (!(fx >= 0.0 && fy >= 0.0 && fz >= 0.0 && fx < (double)g.n[0] && fy < (double)g.n[1] && fz < (double)g.n[2]))
+    return false;
+  const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
+  const int k = (int)g.k[(iz * g.n[1] + iy) * g.n[0] + ix];
+  return (double)(k - 2) * g.h_free > max_t;
 }
 // Sphere::test + the range checks of Sphere::intersect (sphere.cpp:10-53), min_t = 0
 __device__ __forceinline__ bool sphere_t(v3 c, double r2, v3 o, v3 d, double max_t, double& t) {
@@ -227,6 +258,116 @@ __device__ __forceinline__ bool traverse(const KParams& kp, v3 o, v3 d, v3 y, do
   return hit;
 }
 
+// Test the primitives of an accepted leaf (slots [first, first + count)), as intersect_micro's
+// leaf loop: every accepted hit shrinks max_t (t <= max_t: a later equal t wins).
+template <bool ANY>
+__device__ __forceinline__ bool leaf_prims(const KParams& kp, int first, int count, v3 o, v3 d, double& max_t,
+                                           int& hit_slot, double& hb1, double& hb2) {
+  bool hit = false;
+  for (int i = 0; i < count; ++i) {
+    const int slot = first + i;
+    const DPrimMeta meta = kp.meta[slot];
+    const DPrimGeo gp = kp.geo[slot];
+    double t, b1 = 0, b2 = 0;
+    const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, max_t, t)
+                                : tri_t(gp, o, d, max_t, t, b1, b2);
+    if (ok) {
+      max_t = t; hit = true; hit_slot = slot; hb1 = b1; hb2 = b2;
+      if (ANY) return true;
+    }
+  }
+  return hit;
+}
+
+// Plane cull: may primitive `slot` accept a segment whose end points lie at signed distances
+// a, b from its supporting plane?  Triangle::intersect accepts only if the segment meets the
+// plane at some t in [0, max_t]; with both ends farther than plane_eps on one side it cannot
+// -- its t is then out of range by far more than rounding (the margin is ~1e6 ulps of the
+// scene scale, and sliver triangles, whose rounding is unbounded, carry n = 0: never culled).
+// max_t only shrinks along the walk, so the segment's first end point b stays valid.
+__device__ __forceinline__ bool plane_may_hit(const DPlane& pl, v3 o, v3 e, double eps) {
+  const double a = (pl.n[0] * o.x + pl.n[1] * o.y + pl.n[2] * o.z) - pl.c;
+  const double b = (pl.n[0] * e.x + pl.n[1] * e.y + pl.n[2] * e.z) - pl.c;
+  return !((a > eps && b > eps) || (a < -eps && b < -eps));
+}
+// leaf_prims with the plane cull in front of every primitive test (skipped primitives are ones
+// the reference tests and rejects, so the answer is the same)
+template <bool ANY>
+__device__ __forceinline__ bool leaf_prims_cull(const KParams& kp, int first, int count, v3 o, v3 d, v3 e,
+                                                double& max_t, int& hit_slot, double& hb1, double& hb2) {
+  bool hit = false;
+  for (int i = 0; i < count; ++i) {
+    const int slot = first + i;
+    if (!plane_may_hit(kp.planes[slot], o, e, kp.plane_eps)) continue;
+    const DPrimMeta meta = kp.meta[slot];
+    const DPrimGeo gp = kp.geo[slot];
+    double t, b1 = 0, b2 = 0;
+    const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, max_t, t)
+                                : tri_t(gp, o, d, max_t, t, b1, b2);
+    if (ok) {
+      max_t = t; hit = true; hit_slot = slot; hb1 = b1; hb2 = b2;
+      if (ANY) return true;
+    }
+  }
+  return hit;
+}
+// Does any primitive of the leaf survive the plane cull?
+__device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int count, v3 o, v3 e) {
+  bool any = false;
+  for (int i = 0; i < count; ++i) any |= plane_may_hit(kp.planes[first + i], o, e, kp.plane_eps);
+  return any;
+}
+
+// The same result as traverse(), over the "clean" tree (rrt_host.cpp build_clean_tree).
+// Why it is the same: the slab test is monotone under box inclusion (every quotient
+// RN((m - o) / d) is monotone in m), so a leaf's box passing implies every ancestor's box passes
+// at the ancestor's (earlier, larger-or-equal) max_t.  Hence the reference tests a leaf's
+// primitives exactly when that leaf's own box passes with the max_t left by the leaves before it
+// in left-first order -- inner boxes only prune.  So any walk that offers every leaf whose box
+// could pass, in left-first order, to the exact leaf test gives the reference's answer.  The
+// clean tree is the reference tree without its few oversized leaves (Cornell-box walls and
+// lights, whose boxes span the room and inflate every ancestor), with inner boxes refit to what
+// is left; the oversized leaves are tested directly from a short list, merged in by their
+// left-first ordinal.  The reference's root test comes first, so rays outside the scene still
+// cost one box test.
+template <bool ANY, bool EXACT>
+__device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
+                                               double& hb1, double& hb2) {
+  if (!slab<EXACT>(kp.nodes[0], o, d, y, max_t)) return false;
+  const v3 e = o + vmul(d, max_t);  // far end point (cull only; max_t only shrinks below)
+  bool hit = false;
+  int bi = 0;
+  const int nb = (int)kp.n_big;
+  int next_big = nb ? kp.big[0].dfs : 0x7fffffff;
+  int node = kp.clean_root;
+  for (;;) {
+    const bool more = node >= 0;
+    DNode n;
+    if (more) n = kp.clean_nodes[node];
+    const int lim = more ? n.pad : 0x7fffffff;  // pad = left-first ordinal of the subtree's first leaf
+    while (next_big < lim) {                    // oversized leaves that come first
+      const DBig& bg = kp.big[bi];
+      // primitives first: an oversized leaf's box (the room) passes for almost every segment
+      if (leaf_may_hit(kp, bg.first, bg.count, o, e) && slab<EXACT>(bg.mn, bg.mx, o, d, y, max_t) &&
+          leaf_prims_cull<ANY>(kp, bg.first, bg.count, o, d, e, max_t, hit_slot, hb1, hb2)) {
+        hit = true;
+        if (ANY) return true;
+      }
+      ++bi;
+      next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
+    }
+    if (!more) break;
+    if (!slab<EXACT>(n, o, d, y, max_t)) { node = n.skip; continue; }
+    if (n.count == 0) { node = node + 1; continue; }
+    if (leaf_prims_cull<ANY>(kp, n.first, n.count, o, d, e, max_t, hit_slot, hb1, hb2)) {
+      hit = true;
+      if (ANY) return true;
+    }
+    node = n.skip;
+  }
+  return hit;
+}
+
 // BlackHole::next_micro_ray (blackhole.cpp:17-40); f4 is computed but unused there
 __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
   v3 no = o + vmul(d, max_t);
@@ -259,19 +400,46 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
 // ignored, as in the reference).  Capture by the hole returns "no hit".
 template <bool ANY, bool COUNT>
 __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  if (COUNT) cn.query++;
+  if (COUNT && !(kp.diag & 2)) cn.query++;
+  RRT_T0(tq0);
   double max_t = 0.0;
   const v3 hc = V(kp.hole.c[0], kp.hole.c[1], kp.hole.c[2]);
   for (int j = 0; j < kp.hole.steps; ++j) {
+    RRT_T0(tm0);
     next_micro(kp.hole, o, d, max_t);
+    RRT_ACC(t_micro, tm0);
     if (COUNT) cn.micro++;
     double tc;
-    if (sphere_t(hc, kp.hole.r2, o, d, max_t, tc)) return false;  // captured
+    if (sphere_t(hc, kp.hole.r2, o, d, max_t, tc)) {  // captured
+      RRT_ACC(t_query, tq0);
+      return false;
+    }
+    if (!COUNT && segment_clear(kp.grid, o, max_t)) continue;  // no primitive within reach
+    if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
+      const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
+                      o.y <= kp.nodes[0].mx[1] && o.z >= kp.nodes[0].mn[2] && o.z <= kp.nodes[0].mx[2];
+      if ((kp.diag & 1) || ((kp.diag & 4) && in) || ((kp.diag & 8) && !in)) continue;
+    }
+    bool clear_diag = false;
+    if (COUNT && (kp.diag & 2)) {  // diagnostic: query slot = clear segments, prim = AABB tests left
+      clear_diag = segment_clear(kp.grid, o, max_t);
+      if (clear_diag) cn.query++;
+    }
+    const uint32_t bbox_before = cn.bbox, prim_before = cn.prim;
     int slot = -1;
     double b1 = 0, b2 = 0, seg_t = max_t;
     const v3 y = V(xdiv(1.0, d.x), xdiv(1.0, d.y), xdiv(1.0, d.z));
-    const bool hit = segment_fast(kp, o, d) ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
-                                            : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
+    const bool fast = segment_fast(kp, o, d);
+    RRT_T0(tt0);
+    bool hit;
+    if (!COUNT && kp.clean_nodes)
+      hit = fast ? traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2)
+                 : traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2);
+    else
+      hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
+                 : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
+    RRT_ACC(t_trav, tt0);
+    if (COUNT && (kp.diag & 2)) cn.prim = prim_before + (clear_diag ? 0u : cn.bbox - bbox_before);
     if (hit) {
       if (!ANY) {
         const DPrimMeta meta = kp.meta[slot];
@@ -288,9 +456,11 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
                   smul(b2, V(nn.n[6], nn.n[7], nn.n[8]));
         }
       }
+      RRT_ACC(t_query, tq0);
       return true;
     }
   }
+  RRT_ACC(t_query, tq0);
   return false;
 }
 

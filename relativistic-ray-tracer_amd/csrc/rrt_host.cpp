@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -23,6 +24,7 @@ hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, i
                              hipStream_t stream);
 hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_sample(const KParams& kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -87,6 +89,9 @@ struct rrt_ctx {
   uint32_t max_depth = 0;
   bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (qdiv, rrt_device.h)
   bool lean = false;      // area lights only and no microfacet BSDF (LEAN kernel builds)
+  uint32_t grid_res = 128;  // empty-space grid cells along the longest root-box axis (<= 1: none)
+  std::vector<uint8_t> grid;
+  DGrid hgrid{};           // host copy (k = nullptr)
   std::vector<DBsdf> bsdfs;
   std::vector<DLight> lights;
   bool has_scene = false, has_camera = false;
@@ -99,6 +104,16 @@ struct rrt_ctx {
   DPrimMeta* d_meta = nullptr;
   DBsdf* d_bsdfs = nullptr;
   DLight* d_lights = nullptr;
+  uint8_t* d_grid = nullptr;
+  DNode* d_clean = nullptr;
+  DPlane* d_planes = nullptr;
+  double plane_eps = 0;
+  DBig* d_big = nullptr;
+  int32_t clean_root = -1;
+  uint32_t n_big = 0;
+  bool has_clean = false;
+  std::vector<DNode> clean;  // host copies (rrt_get_clean_tree)
+  std::vector<DBig> big;
   uint64_t device_bytes = 0;
   // per-launch workspace
   uint32_t* d_counter = nullptr;
@@ -124,7 +139,8 @@ static int fail(rrt_ctx* c, int code, const std::string& msg) {
 static void free_scene_dev(rrt_ctx* c) {
   if (c->device < 0) return;
   hipFree(c->d_nodes); hipFree(c->d_geo); hipFree(c->d_nrm); hipFree(c->d_meta); hipFree(c->d_bsdfs);
-  hipFree(c->d_lights);
+  hipFree(c->d_lights); hipFree(c->d_grid); hipFree(c->d_clean); hipFree(c->d_big); hipFree(c->d_planes);
+  c->d_grid = nullptr; c->d_clean = nullptr; c->d_big = nullptr; c->d_planes = nullptr;
   c->d_nodes = nullptr; c->d_geo = nullptr; c->d_nrm = nullptr; c->d_meta = nullptr; c->d_bsdfs = nullptr;
   c->d_lights = nullptr;
   c->device_bytes = 0;
@@ -138,6 +154,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
   if (!out) return RRT_E_INVALID;
   std::unique_ptr<rrt_ctx> c(new rrt_ctx());
   c->device = cfg ? cfg->device : 0;
+  if (cfg && cfg->free_grid_res) c->grid_res = std::min<uint32_t>(cfg->free_grid_res, 1024);
   // default spacetime: global_black_hole (blackhole.cpp:5)
   rrt_spacetime_desc st{};
   st.kind = RRT_METRIC_SCHWARZSCHILD; st.center[1] = 1.0; st.r_s = 0.1; st.delta_theta = 0.1;
@@ -229,6 +246,194 @@ static int build(rrt_ctx* c, const std::vector<uint32_t>& ids, uint32_t depth) {
   c->nodes[me].left = l;
   c->nodes[me].right = r;
   return me;
+}
+
+// Empty-space grid (DGrid, rrt_internal.h).  Cubic cells of size h over the root box.  A cell is
+// "occupied" if some primitive could report a hit for a segment passing through it:
+//  * sphere: its bounding box;
+//  * triangle: the part of its leaf's box within one cell of the triangle's plane.  In exact
+//    arithmetic a hit lies on the triangle; in floating point Triangle::intersect can also
+//    accept a segment that is parallel to the plane to within rounding (det, t and both
+//    barycentric numerators all vanish), anywhere along the plane -- but only inside the leaf
+//    box, because the leaf's slab test gates every primitive test;
+//  * sliver triangle (|e1 x e2| < 1e-6 |e1| |e2|): its whole leaf box.
+// Every range is widened by one cell per side.  A multi-source BFS over the 26-neighbourhood
+// then gives each cell its Chebyshev distance k (in cells, capped at 255) to the nearest
+// occupied cell.  A point p whose computed cell is c lies in a true cell c* with |c - c*| <= 1
+// (rounding of (p - g0) / h); any point q of a hit region lies in an occupied cell c_q, so
+// |c* - c_q|_inf >= k - 1 and |p - q| >= |p - q|_inf >= (k - 2) h.  A segment shorter than that
+// stays about a cell (~1e13 ulps) away from every hit region, so no primitive accepts it.
+static void build_free_grid(rrt_ctx* c) {
+  c->grid.clear();
+  c->hgrid = DGrid{};
+  if (c->grid_res <= 1 || c->nodes.empty()) return;
+  const Box& rb = c->nodes[0].bb;
+  const double ext[3] = {rb.ext.x, rb.ext.y, rb.ext.z}, g0[3] = {rb.mn.x, rb.mn.y, rb.mn.z};
+  const double emax = std::max(ext[0], std::max(ext[1], ext[2]));
+  if (!(emax > 0) || !std::isfinite(emax)) return;
+  for (double v : g0) if (!std::isfinite(v)) return;
+  const double h = emax / c->grid_res, inv_h = 1.0 / h;
+  int32_t n[3];
+  for (int i = 0; i < 3; ++i) n[i] = (int32_t)std::floor(ext[i] * inv_h) + 2;
+  const size_t total = (size_t)n[0] * n[1] * n[2];
+  std::vector<uint8_t> k(total, 255);
+  std::vector<uint32_t> q;
+  q.reserve(total / 4);
+  auto idx = [&](int x, int y, int z) { return ((size_t)z * n[1] + y) * n[0] + x; };
+  auto mark = [&](int x, int y, int z) {
+    const size_t i = idx(x, y, z);
+    if (k[i] != 0) { k[i] = 0; q.push_back((uint32_t)i); }
+  };
+  // cell range of [mn, mx] widened by one cell; false if not finite
+  auto range = [&](const V3& mn, const V3& mx, int lo[3], int hi[3]) {
+    const double a[3] = {mn.x, mn.y, mn.z}, b[3] = {mx.x, mx.y, mx.z};
+    for (int i = 0; i < 3; ++i) {
+      if (!std::isfinite(a[i]) || !std::isfinite(b[i])) return false;
+      lo[i] = std::max(0, (int)std::floor((a[i] - g0[i]) * inv_h) - 1);
+      hi[i] = std::min(n[i] - 1, (int)std::floor((b[i] - g0[i]) * inv_h) + 1);
+    }
+    return true;
+  };
+  const double reach = h * (std::sqrt(3.0) / 2 + 1.0);  // cell centre to plane: within one cell
+  for (const BNode& nd : c->nodes) {
+    if (nd.count == 0) continue;
+    int llo[3], lhi[3];
+    if (!range(nd.bb.mn, nd.bb.mx, llo, lhi)) { c->grid.clear(); return; }
+    for (int j = 0; j < nd.count; ++j) {
+      const Prim& p = c->prims[c->leaf[nd.first + j]];
+      int lo[3], hi[3];
+      if (p.kind == RRT_OBJ_SPHERE) {
+        const Box b = prim_box(c, p);
+        if (!range(b.mn, b.mx, lo, hi)) { c->grid.clear(); return; }
+        for (int z = lo[2]; z <= hi[2]; ++z)
+          for (int y = lo[1]; y <= hi[1]; ++y)
+            for (int x = lo[0]; x <= hi[0]; ++x) mark(x, y, z);
+        continue;
+      }
+      const V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
+      const V3 nn = mk(e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x);
+      const double nl = std::sqrt(nn.x * nn.x + nn.y * nn.y + nn.z * nn.z);
+      const double l1 = std::sqrt(e1.x * e1.x + e1.y * e1.y + e1.z * e1.z);
+      const double l2 = std::sqrt(e2.x * e2.x + e2.y * e2.y + e2.z * e2.z);
+      const bool sliver = !(nl >= 1e-6 * l1 * l2) || !std::isfinite(nl);
+      for (int z = llo[2]; z <= lhi[2]; ++z)
+        for (int y = llo[1]; y <= lhi[1]; ++y)
+          for (int x = llo[0]; x <= lhi[0]; ++x) {
+            if (!sliver) {
+              const double cx = g0[0] + (x + 0.5) * h, cy = g0[1] + (y + 0.5) * h, cz = g0[2] + (z + 0.5) * h;
+              const double dist = std::fabs(nn.x * (cx - p0.x) + nn.y * (cy - p0.y) + nn.z * (cz - p0.z)) / nl;
+              if (dist > reach) continue;
+            }
+            mark(x, y, z);
+          }
+    }
+  }
+  for (size_t head = 0; head < q.size(); ++head) {  // BFS: Chebyshev distance transform
+    const uint32_t i = q[head];
+    const int x = (int)(i % n[0]), y = (int)((i / n[0]) % n[1]), z = (int)(i / ((size_t)n[0] * n[1]));
+    const int nk = k[i] + 1;
+    if (nk >= 255) continue;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int xx = x + dx, yy = y + dy, zz = z + dz;
+          if (xx < 0 || yy < 0 || zz < 0 || xx >= n[0] || yy >= n[1] || zz >= n[2]) continue;
+          const size_t j = idx(xx, yy, zz);
+          if (k[j] > nk) { k[j] = (uint8_t)nk; q.push_back((uint32_t)j); }
+        }
+  }
+  c->grid.swap(k);
+  DGrid& g = c->hgrid;
+  for (int i = 0; i < 3; ++i) { g.g0[i] = g0[i]; g.n[i] = n[i]; }
+  g.inv_h = inv_h;
+  g.h_free = h * (1.0 - 0x1p-20);
+}
+
+// Clean tree for traverse_clean (rrt_device.h): the reference tree without its oversized leaves,
+// inner boxes refit to the leaves left, in left-first pre-order with skip pointers; DNode.pad
+// holds the left-first ordinal of the subtree's first leaf.  Oversized = box diagonal above
+// 8x the median leaf diagonal (at most 64 leaves, the largest first; none if that would leave
+// no tree).  Leaf boxes are the reference's own.
+static void build_clean_tree(rrt_ctx* c, std::vector<DNode>& out, std::vector<DBig>& big) {
+  out.clear(); big.clear();
+  c->has_clean = false; c->clean_root = -1; c->n_big = 0;
+  const size_t nn = c->nodes.size();
+  if (nn == 0) return;
+  std::vector<int32_t> ordinal(nn, -1);
+  std::vector<double> diag;
+  int32_t nl = 0;
+  for (size_t i = 0; i < nn; ++i)
+    if (c->nodes[i].count != 0) {
+      ordinal[i] = nl++;
+      const V3 e = c->nodes[i].bb.ext;
+      diag.push_back(std::sqrt(e.x * e.x + e.y * e.y + e.z * e.z));
+    }
+  std::vector<double> sorted = diag;
+  std::nth_element(sorted.begin(), sorted.begin() + sorted.size() / 2, sorted.end());
+  const double thresh = 8.0 * sorted[sorted.size() / 2];
+  std::vector<std::pair<double, int32_t>> cand;  // (diagonal, node)
+  for (size_t i = 0; i < nn; ++i)
+    if (c->nodes[i].count != 0 && diag[ordinal[i]] > thresh) cand.push_back({diag[ordinal[i]], (int32_t)i});
+  std::sort(cand.begin(), cand.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  if (cand.size() > 64) cand.resize(64);
+  if (cand.empty() || (int32_t)cand.size() >= nl) return;  // nothing to gain
+  std::vector<char> is_big(nn, 0);
+  for (const auto& pr : cand) is_big[pr.second] = 1;
+  // rebuild: returns the new index of the subtree's clean root, or -1 if nothing is left
+  struct T { Box bb; int32_t first, count, left, right, ord; };
+  std::vector<T> tmp;
+  std::function<int32_t(int32_t)> rec = [&](int32_t i) -> int32_t {
+    const BNode& n = c->nodes[i];
+    if (n.count != 0) {
+      if (is_big[i]) return -1;
+      tmp.push_back(T{n.bb, n.first, n.count, -1, -1, ordinal[i]});
+      return (int32_t)tmp.size() - 1;
+    }
+    const int32_t l = rec(n.left), r = rec(n.right);
+    if (l < 0) return r;
+    if (r < 0) return l;
+    Box b = tmp[l].bb;
+    b.expand(tmp[r].bb);
+    tmp.push_back(T{b, 0, 0, l, r, std::min(tmp[l].ord, tmp[r].ord)});
+    return (int32_t)tmp.size() - 1;
+  };
+  const int32_t root = rec(0);
+  if (root < 0) return;
+  // linearise in pre-order (left first) with skip pointers
+  std::vector<int32_t> order;
+  std::function<void(int32_t)> pre = [&](int32_t i) {
+    order.push_back(i);
+    if (tmp[i].count == 0) { pre(tmp[i].left); pre(tmp[i].right); }
+  };
+  pre(root);
+  std::vector<int32_t> pos(tmp.size());
+  for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (int32_t)k;
+  out.resize(order.size());
+  std::vector<int32_t> skip(order.size(), -1);
+  for (size_t k = 0; k < order.size(); ++k) {
+    const T& t = tmp[order[k]];
+    if (t.count == 0) {
+      skip[pos[t.left]] = pos[t.right];
+      skip[pos[t.right]] = skip[k];
+    }
+  }
+  for (size_t k = 0; k < order.size(); ++k) {
+    const T& t = tmp[order[k]];
+    DNode& d = out[k];
+    d.mn[0] = t.bb.mn.x; d.mn[1] = t.bb.mn.y; d.mn[2] = t.bb.mn.z;
+    d.mx[0] = t.bb.mx.x; d.mx[1] = t.bb.mx.y; d.mx[2] = t.bb.mx.z;
+    d.skip = skip[k]; d.first = t.first; d.count = t.count; d.pad = t.ord;
+  }
+  for (const auto& pr : cand) {
+    const BNode& n = c->nodes[pr.second];
+    DBig b{};
+    b.mn[0] = n.bb.mn.x; b.mn[1] = n.bb.mn.y; b.mn[2] = n.bb.mn.z;
+    b.mx[0] = n.bb.mx.x; b.mx[1] = n.bb.mx.y; b.mx[2] = n.bb.mx.z;
+    b.first = n.first; b.count = n.count; b.dfs = ordinal[pr.second];
+    big.push_back(b);
+  }
+  std::sort(big.begin(), big.end(), [](const DBig& a, const DBig& b) { return a.dfs < b.dfs; });
+  c->has_clean = true; c->clean_root = 0; c->n_big = (uint32_t)big.size();
 }
 
 static int upload(rrt_ctx* c, void** dst, const void* src, size_t bytes) {
@@ -329,6 +534,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   std::vector<DPrimGeo> geo(c->leaf.size());
   std::vector<DPrimNrm> nrm(c->leaf.size());
   std::vector<DPrimMeta> meta(c->leaf.size());
+  std::vector<DPlane> planes(c->leaf.size());
   for (size_t k = 0; k < c->leaf.size(); ++k) {
     const Prim& p = c->prims[c->leaf[k]];
     std::memset(&geo[k], 0, sizeof(DPrimGeo));
@@ -342,11 +548,31 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
         nrm[k].n[3 * j] = n.x; nrm[k].n[3 * j + 1] = n.y; nrm[k].n[3 * j + 2] = n.z;
       }
       meta[k] = (p.bsdf << 8);
+      // supporting plane for the cull (rrt_device.h plane_may_hit); slivers never cull
+      const V3 nn = mk(e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x);
+      const double nl = std::sqrt(nn.x * nn.x + nn.y * nn.y + nn.z * nn.z);
+      const double l1 = std::sqrt(e1.x * e1.x + e1.y * e1.y + e1.z * e1.z);
+      const double l2 = std::sqrt(e2.x * e2.x + e2.y * e2.y + e2.z * e2.z);
+      DPlane pl{};
+      if (nl >= 1e-6 * l1 * l2 && std::isfinite(nl)) {
+        pl.n[0] = nn.x / nl; pl.n[1] = nn.y / nl; pl.n[2] = nn.z / nl;
+        pl.c = pl.n[0] * p0.x + pl.n[1] * p0.y + pl.n[2] * p0.z;
+      }
+      planes[k] = pl;
     } else {
       double g[9] = {p.c.x, p.c.y, p.c.z, p.r2, p.r, 0, 0, 0, 0};
       std::memcpy(geo[k].v, g, sizeof(g));
       meta[k] = (p.bsdf << 8) | 1u;
     }
+  }
+  build_free_grid(c);
+  build_clean_tree(c, c->clean, c->big);
+  {  // plane-cull margin: 1e-9 of the scene's coordinate scale (rounding is ~1e-16 of it)
+    const Box& rb = c->nodes[0].bb;
+    double m = 1.0;
+    for (double v : {rb.mn.x, rb.mn.y, rb.mn.z, rb.mx.x, rb.mx.y, rb.mx.z}) m = std::max(m, std::fabs(v));
+    c->plane_eps = std::isfinite(m) ? 1e-9 * m : 0.0;
+    if (c->plane_eps == 0.0) for (DPlane& pl : planes) pl = DPlane{};  // never cull
   }
   c->lean = true;
   for (const DLight& l : c->lights) if (l.type != RRT_LIGHT_AREA) c->lean = false;
@@ -362,6 +588,12 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if ((rc = upload(c, (void**)&c->d_meta, meta.data(), meta.size() * sizeof(DPrimMeta)))) return rc;
   if ((rc = upload(c, (void**)&c->d_bsdfs, c->bsdfs.data(), c->bsdfs.size() * sizeof(DBsdf)))) return rc;
   if ((rc = upload(c, (void**)&c->d_lights, c->lights.data(), c->lights.size() * sizeof(DLight)))) return rc;
+  if (!c->grid.empty() && (rc = upload(c, (void**)&c->d_grid, c->grid.data(), c->grid.size()))) return rc;
+  if ((rc = upload(c, (void**)&c->d_planes, planes.data(), planes.size() * sizeof(DPlane)))) return rc;
+  if (c->has_clean) {
+    if ((rc = upload(c, (void**)&c->d_clean, c->clean.data(), c->clean.size() * sizeof(DNode)))) return rc;
+    if ((rc = upload(c, (void**)&c->d_big, c->big.data(), c->big.size() * sizeof(DBig)))) return rc;
+  }
   return RRT_OK;
 }
 
@@ -444,9 +676,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size();
   kp.fast_div = (c->fast_div && !(p->flags & RRT_RENDER_EXACT_DIV)) ? 1u : 0u;
   kp.cam = c->cam; kp.hole = c->hole;
+  kp.grid = c->hgrid;
+  kp.grid.k = (p->flags & RRT_RENDER_NO_SKIP) ? nullptr : c->d_grid;
+  const bool use_clean = c->has_clean && !(p->flags & RRT_RENDER_NO_CLEAN);
+  kp.clean_nodes = use_clean ? c->d_clean : nullptr;
+  kp.big = c->d_big; kp.clean_root = c->clean_root; kp.n_big = c->n_big;
+  kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
   kp.direct_hemisphere = p->direct_hemisphere; kp.seed = p->seed;
+  kp.diag = (p->flags >> 30) | ((p->flags >> 26) & 12u);
   kp.frame_w = (double)p->frame_w; kp.frame_h = (double)p->frame_h;
   kp.frame_wi = p->frame_w; kp.frame_hi = p->frame_h;
   kp.tiles = c->d_tiles; kp.n_tiles = n_tiles; kp.tile_size = ts;
@@ -464,16 +703,44 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
   const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
   const int lean = (!deep && !count && c->lean && !p->direct_hemisphere) ? 1 : 0;
-  const int waves = (p->variant >= 1 && p->variant <= 5) ? (int)p->variant : (pixel_loop || mega ? 2 : 3);
+  const uint32_t wv = p->variant & 0xffu;
+  const int waves = (wv >= 1 && wv <= 5) ? (int)wv : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
-  uint32_t want = (kp.n_blocks + 3) / 4;
+  // Sample-parallel kernel (rrt_sample.hip rrt_batch_kernel) whenever a pixel takes more than
+  // one sample: it needs each camera sample's RNG draw count to depend only on whether its query
+  // hit, which holds at depth <= 1 (jitter + the direct-lighting samplers).
+  const bool batch = !deep && !count && !mega && !pixel_loop && p->ns_aa >= 2 && !(p->flags & RRT_RENDER_PER_PIXEL);
+  if (batch) {
+    kp.draws_miss = 2;
+    uint32_t dh = 2;
+    if (p->max_ray_depth >= 1) {
+      if (p->direct_hemisphere) {
+        dh += 2u * (uint32_t)c->lights.size() * p->ns_area_light;
+      } else {
+        for (const DLight& l : c->lights) {
+          const uint32_t num = l.is_delta ? 1u : p->ns_area_light;
+          const bool sampled = l.type == RRT_LIGHT_AREA || l.type == RRT_LIGHT_HEMISPHERE;  // 2 draws each
+          dh += sampled ? 2u * num : 0u;
+        }
+      }
+    }
+    kp.draws_hit = dh;
+    uint32_t gsz = 2;
+    const uint32_t want_g = std::min<uint32_t>(std::min<uint32_t>(p->ns_aa, p->samples_per_batch), 32u);
+    while (gsz < want_g) gsz <<= 1;
+    kp.group = gsz;
+    kp.n_pixels = n_tiles * ts * ts;
+  }
+  uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (grid == 0) grid = 1;
   c->last_grid = grid;
   HIPCHK(c, hipEventRecord(c->ev0, stream));
-  if (mega)
+  if (batch)
+    HIPCHK(c, rrt_launch_batch(kp, lean, waves, grid, stream));
+  else if (mega)
     HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
   else if (pixel_loop)
     HIPCHK(c, rrt_launch_render(kp, deep, count, lean, waves, grid, stream));
@@ -584,6 +851,14 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
   out->max_depth = c->max_depth;
   out->device_bytes = c->device_bytes;
   out->grid_blocks = c->last_grid;
+  out->n_clean = c->has_clean ? (uint32_t)c->clean.size() : 0u;
+  out->n_big = c->has_clean ? (uint32_t)c->big.size() : 0u;
+  if (!c->grid.empty()) {
+    for (int i = 0; i < 3; ++i) out->grid_n[i] = (uint32_t)c->hgrid.n[i];
+    size_t free_cells = 0;
+    for (uint8_t v : c->grid) free_cells += v > 2;
+    out->grid_free_frac = (float)((double)free_cells / (double)c->grid.size());
+  }
   out->block_threads = 256;
   if (c->device >= 0 && c->timed) {
     hipSetDevice(c->device);
@@ -594,6 +869,35 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
   }
   out->last_kernel_ms = c->last_ms;
   return RRT_OK;
+}
+
+extern "C" int rrt_get_free_grid(const rrt_ctx* c, uint8_t* k, double* geom, int32_t* n) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  if (c->grid.empty()) return 0;
+  if (k) std::memcpy(k, c->grid.data(), c->grid.size());
+  if (geom) {
+    for (int i = 0; i < 3; ++i) geom[i] = c->hgrid.g0[i];
+    geom[3] = c->hgrid.inv_h; geom[4] = c->hgrid.h_free;
+  }
+  if (n) for (int i = 0; i < 3; ++i) n[i] = c->hgrid.n[i];
+  return (int)std::min<size_t>(c->grid.size(), 0x7fffffff);
+}
+
+extern "C" int rrt_get_clean_tree(const rrt_ctx* c, double* boxes, int32_t* nodes, double* big_boxes,
+                                  int32_t* big) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  if (!c->has_clean) return 0;
+  for (size_t i = 0; i < c->clean.size(); ++i) {
+    const DNode& n = c->clean[i];
+    if (boxes) for (int k = 0; k < 3; ++k) { boxes[6 * i + k] = n.mn[k]; boxes[6 * i + 3 + k] = n.mx[k]; }
+    if (nodes) { nodes[4 * i] = n.skip; nodes[4 * i + 1] = n.first; nodes[4 * i + 2] = n.count; nodes[4 * i + 3] = n.pad; }
+  }
+  for (size_t i = 0; i < c->big.size(); ++i) {
+    const DBig& b = c->big[i];
+    if (big_boxes) for (int k = 0; k < 3; ++k) { big_boxes[6 * i + k] = b.mn[k]; big_boxes[6 * i + 3 + k] = b.mx[k]; }
+    if (big) { big[3 * i] = b.first; big[3 * i + 1] = b.count; big[3 * i + 2] = b.dfs; }
+  }
+  return (int)c->clean.size();
 }
 
 extern "C" int rrt_get_bvh(const rrt_ctx* c, double* boxes, int32_t* nodes, uint32_t* prims) {

@@ -21,10 +21,21 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 64, "DNode must be 64 bytes");
 
+// Oversized leaf of the reference tree, tested directly by the clean-tree walk
+// (rrt_device.h traverse_clean): its box, leaf slots and left-first leaf ordinal.
+struct alignas(16) DBig {
+  double mn[3];
+  double mx[3];
+  int32_t first, count, dfs, pad;
+};
+
 // Leaf-slot geometry, 72 B (9 doubles) per slot, slots in leaf order.
 //   triangle: p0, e1 = p1 - p0, e2 = p2 - p0 (exactly the values triangle.cpp:31-32 computes)
 //   sphere:   c.x, c.y, c.z, r2, r, 0...
 struct DPrimGeo { double v[9]; };
+// Leaf-slot supporting plane (unit normal n, offset c = n . p0) for the cull in
+// rrt_device.h leaf_prims; n = 0, c = 0 (never culls) for spheres and sliver triangles.
+struct DPlane { double n[3]; double c; };
 // Leaf-slot shading data: vertex normals n0, n1, n2 (triangle) -- read only on an accepted hit.
 struct DPrimNrm { double n[9]; };
 // Leaf-slot metadata: bit 0 = sphere, bits 8..15 = bsdf index.
@@ -53,6 +64,21 @@ struct DHole {
   int32_t pad;
 };
 
+// Empty-space grid over the root box (rrt_host.cpp build_free_grid): cell value k = Chebyshev
+// distance, in cells, to the nearest cell touched by a BVH leaf box (cells of leaf boxes
+// widened by one, capped at 255).  Every point of cell c lies at least (k - 2) * h from every
+// leaf box, so a micro segment starting in c that is shorter than that reaches no leaf box:
+// every leaf slab test fails, no primitive is tested, and the reference's traversal returns
+// "no hit" -- the traversal can be skipped without changing any result.
+struct DGrid {
+  const uint8_t* k;   // [n[2]][n[1]][n[0]]; null = no grid
+  double g0[3];       // root box minimum
+  double inv_h;       // 1 / cell size
+  double h_free;      // cell size * (1 - 2^-20): the free radius of value k is (k - 2) * h_free
+  int32_t n[3];
+  int32_t pad;
+};
+
 struct KParams {
   // scene
   const DNode* nodes;
@@ -63,12 +89,20 @@ struct KParams {
   const DLight* lights;
   uint32_t n_lights;
   uint32_t fast_div;  // scene bounds allow the Markstein-corrected slab quotients (rrt_mega.hip)
+  DGrid grid;
+  const DNode* clean_nodes;   // clean tree (pad = first leaf ordinal); null: reference walk only
+  const DPlane* planes;       // per leaf slot; null: no plane cull
+  double plane_eps;           // plane-cull margin (scene-scaled, ~1e6 x rounding error)
+  const DBig* big;            // oversized leaves by left-first ordinal
+  int32_t clean_root;         // 0, or -1 if every leaf is oversized
+  uint32_t n_big;
   DCamera cam;
   DHole hole;
   // render
   uint32_t ns_aa, max_ray_depth, ns_area_light, samples_per_batch;
   float max_tolerance;
   uint32_t direct_hemisphere;
+  uint32_t diag;  // RRT_RENDER_DIAG_* bits >> 30 (bit 0: no traversal, bit 1: clear-segment stats)
   uint64_t seed;
   double frame_w, frame_h;
   uint32_t frame_wi, frame_hi;
@@ -77,6 +111,11 @@ struct KParams {
   uint32_t n_tiles, tile_size;
   uint32_t blocks_per_tile_side, n_blocks;
   uint32_t* block_counter;
+  // sample-parallel kernel (rrt_sample.hip rrt_batch_kernel)
+  uint32_t n_pixels;     // n_tiles * tile_size^2 (pixel work items)
+  uint32_t group;        // lanes per pixel (power of two, 2..32)
+  uint32_t draws_miss;   // RNG draws of a camera sample whose query misses (jitter: 2)
+  uint32_t draws_hit;    // ... and of one that hits (jitter + the direct-lighting sampler draws)
   uint32_t clip_x0, clip_y0, clip_x1, clip_y1;  // region actually requested (exclusive end)
   // outputs, packed per tile: pixel (i, j) of tile t at t*tile_size^2 + j*tile_size + i
   float* rgb;

@@ -12,10 +12,16 @@
 namespace rrt {
 
 // ------------------------------------------------------------------ integrator (part1_code.cpp)
+// `trace` = the geodesic-marched BVH query; DEEP (bounce) builds and depth <= 1 builds share it.
+template <bool ANY, bool COUNT, bool DEEP>
+__device__ __forceinline__ bool trace(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  return query<ANY, COUNT>(kp, o, d, is, cn);
+}
+
 // LEAN: area lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
 // (same values: make_coord_space is a pure function of the normal) instead of being kept live
 // across the shadow query, which keeps 12 VGPRs out of the traversal loop.
-template <bool COUNT, bool LEAN>
+template <bool COUNT, bool LEAN, bool DEEP>
 __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :33-57
   const DBsdf b = kp.bsdfs[is.bsdf];
   spec L = S(0, 0, 0);
@@ -31,13 +37,13 @@ __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Co
       v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
       spec contrib = ((sample * bsdf_f<LEAN>(b, to_local(f, is.w_out), w_in)) * (float)w_in.z) / pdf;
-      if (!query<true, COUNT>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
+      if (!trace<true, COUNT, DEEP>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
     }
   }
   return L / (float)total;
 }
 
-template <bool COUNT>
+template <bool COUNT, bool DEEP>
 __device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :15-31
   Frame f = coord_space(is.n);
   v3 w_out = to_local(f, is.w_out);
@@ -48,16 +54,17 @@ __device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Co
     v3 w_in = hemisphere_sample(g);
     v3 wi_world = to_world(f, w_in);
     Isect is2;
-    if (query<false, COUNT>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (trace<false, COUNT, DEEP>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * bsdf_f(b, w_out, w_in)) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
 }
 
-template <bool COUNT, bool LEAN = false>
+template <bool COUNT, bool LEAN, bool DEEP>
 __device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {
-  if (LEAN) return direct_importance<COUNT, true>(kp, g, is, cn);
-  return kp.direct_hemisphere ? direct_hemisphere<COUNT>(kp, g, is, cn) : direct_importance<COUNT, false>(kp, g, is, cn);
+  if (LEAN) return direct_importance<COUNT, true, DEEP>(kp, g, is, cn);
+  return kp.direct_hemisphere ? direct_hemisphere<COUNT, DEEP>(kp, g, is, cn)
+                              : direct_importance<COUNT, false, DEEP>(kp, g, is, cn);
 }
 
 // at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
@@ -74,7 +81,7 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
     v3 w_out = to_local(f, cur.w_out);
     const DBsdf b = kp.bsdfs[cur.bsdf];
     spec L_out = S(0, 0, 0);
-    if (!is_delta(b)) L_out = L_out + one_bounce<COUNT>(kp, g, cur, cn);
+    if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, false, true>(kp, g, cur, cn);
     Ld[k] = L_out;
     child[k] = false;
     dl[k] = is_delta(b);
@@ -84,7 +91,7 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
       if (pdf == 0.0f) break;
       v3 wi_world = to_world(f, w_in);
       Isect is2;
-      if (query<false, COUNT>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
+      if (trace<false, COUNT, true>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
         child[k] = true;
         smp[k] = sample; cs[k] = (float)fabs(w_in.z); pd[k] = pdf;
         cem[k] = emission(kp.bsdfs[is2.bsdf]);
@@ -111,10 +118,10 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
 template <bool DEEP, bool COUNT, bool LEAN>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
-  if (!query<false, COUNT>(kp, o, d, &is, cn)) return S(0, 0, 0);
+  if (!trace<false, COUNT, DEEP>(kp, o, d, &is, cn)) return S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
-  if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN>(kp, g, is, cn);
+  if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
   return e + at_least_one_bounce<COUNT>(kp, g, is, cn);
 }
 
@@ -122,10 +129,11 @@ __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3
 template <bool DEEP, bool COUNT, bool LEAN>
 __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
   spec ret = S(0, 0, 0);
-  int i;
+  int n = 0;  // samples taken (the reference's i after its loop; counted explicitly: the
+              // `++i; break;` form was miscompiled in the register-starved bounce build)
   double s1 = 0.0, s2 = 0.0;
   const DCamera& cam = kp.cam;
-  for (i = 0; i < (int)kp.ns_aa; ++i) {
+  for (int i = 0; i < (int)kp.ns_aa; ++i) {
     double sx = (double)x, sy = (double)y;
     if (kp.ns_aa == 1) { sx += 0.5; sy += 0.5; }
     else { double jx, jy; g.grid(jx, jy); sx += jx; sy += jy; }
@@ -138,13 +146,14 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
     double il = illum(s);
     s1 += il;
     s2 += il * il;
-    if ((uint32_t)(i + 1) % kp.samples_per_batch == 0) {
-      double avg = s1 / (i + 1), sd = sqrt((s2 - avg * s1) / i);
-      if (1.96 * sd / sqrt((double)(i + 1)) <= (double)kp.max_tolerance * avg) { ++i; break; }
+    n = i + 1;
+    if ((uint32_t)n % kp.samples_per_batch == 0) {
+      double avg = s1 / n, sd = sqrt((s2 - avg * s1) / i);
+      if (1.96 * sd / sqrt((double)n) <= (double)kp.max_tolerance * avg) break;
     }
   }
-  count = i;
-  return ret / (float)i;
+  count = n;
+  return ret / (float)n;
 }
 
 }  // namespace rrt

@@ -165,6 +165,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(KParams kp) {
       bool done;
       if (sphere_t(hc, kp.hole.r2, qo, qd, qmax, tc)) {
         done = true;  // captured by the hole: "no hit" (bvh.cpp:107-108)
+      } else if (!COUNT && segment_clear(kp.grid, qo, qmax)) {
+        done = qstep >= kp.hole.steps;  // no leaf box within reach: traversal would miss
       } else {
         const v3 y = V(xdiv(1.0, qd.x), xdiv(1.0, qd.y), xdiv(1.0, qd.z));
         const bool fast = segment_fast(kp, qo, qd);

@@ -90,6 +90,21 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 
 }  // namespace rrt
 
+#if RRT_PROFILE
+__device__ unsigned long long rrt_prof[8];
+__device__ unsigned long long rrt_prof_ends[16384], rrt_prof_starts[16384], rrt_prof_work[16384];
+extern "C" int rrt_prof_read(unsigned long long* out) {  // out: 8 + 3 * 16384
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof), sizeof(rrt_prof)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(rrt_prof_ends), sizeof(rrt_prof_ends)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 8 + 16384, HIP_SYMBOL(rrt_prof_starts), sizeof(rrt_prof_starts)) != hipSuccess)
+    return -1;
+  if (hipMemcpyFromSymbol(out + 8 + 2 * 16384, HIP_SYMBOL(rrt_prof_work), sizeof(rrt_prof_work)) != hipSuccess)
+    return -1;
+  unsigned long long z[8] = {0, 0, 0, 0, ~0ull, 0, 0, ~0ull};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rrt_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // COUNT: per-pixel work counters; LEAN: area lights only, no microfacet BSDF, importance-sampled
 // direct light (the BASELINE scenes); WAVES: register budget (minimum waves per SIMD).
 template <bool COUNT, bool LEAN, int WAVES>
@@ -109,7 +124,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
   uint32_t px = 0, py = 0, slot = 0;
   int i = 0;                              // samples done for the lane's pixel
   Rng g; g.key = 0; g.ctr = 0;
-  Counters cn = {0, 0, 0, 0};
+  Counters cn = {};
+#if RRT_PROFILE
+  const uint64_t t_start = clock64(), w_start = wall_clock64();  // clock64 is per XCD; wall is global
+  uint32_t prof_blocks = 0, prof_samples = 0;
+#endif
 
   for (;;) {
     // ---- refill lanes without a pixel (wave-uniform control flow)
@@ -120,7 +139,16 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(kp.block_counter, 1u);
         b = __shfl(b, 0);
-        if (b >= kp.n_blocks) { pool_empty = true; break; }
+        if (b >= kp.n_blocks) {
+          pool_empty = true;
+#if RRT_PROFILE
+          if (lane == 0) atomicMin(&rrt_prof[3 + 4], (unsigned long long)wall_clock64());  // first exhaustion
+#endif
+          break;
+        }
+#if RRT_PROFILE
+        ++prof_blocks;
+#endif
         pool_blk = b;
         pool_next = 0;
       }
@@ -177,6 +205,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
     const double il = illum(s);
     const double s1 = lget(cl.s1, t) + il, s2 = lget(cl.s2, t) + il * il;
     ++i;
+#if RRT_PROFILE
+    ++prof_samples;
+#endif
     bool stop = i >= (int)kp.ns_aa;
     if ((uint32_t)i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
       const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
@@ -197,6 +228,180 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
       lput(cl.rr, t, ret.r); lput(cl.rg, t, ret.g); lput(cl.rb, t, ret.b);
     }
   }
+#if RRT_PROFILE
+  // wave time per phase ~ the busiest lane's; summed over waves (tools/phase_profile.py)
+  const uint64_t t_end = clock64(), w_end = wall_clock64();
+  uint64_t v[4] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav};
+  for (int k = 0; k < 4; ++k) {
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o2 = __shfl_xor(v[k], off);
+      v[k] = v[k] > o2 ? v[k] : o2;
+    }
+    if (lane == 0) atomicAdd(&rrt_prof[k], (unsigned long long)v[k]);
+  }
+  uint32_t ns = prof_samples;
+  for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off);
+  if (lane == 0) {  // [4] min start, [5] max end, [6] waves, [7] first exhaustion; per-wave records
+    atomicMin(&rrt_prof[4], (unsigned long long)w_start);
+    atomicMax(&rrt_prof[5], (unsigned long long)w_end);
+    const unsigned long long w = atomicAdd(&rrt_prof[6], 1ull) & 16383;
+    rrt_prof_ends[w] = w_end;
+    rrt_prof_starts[w] = w_start;
+    rrt_prof_work[w] = ((unsigned long long)prof_blocks << 32) | ns;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// rrt_batch_kernel -- sample-parallel depth <= 1 path: a group of G lanes renders G consecutive
+// camera samples of ONE pixel at a time (G = samples_per_batch rounded up to a power of two, at
+// most 32), so a pixel's 32..64 samples take two group steps instead of 64 sequential lane
+// steps, and the lanes of a group march almost identical (jittered) rays.
+//
+// The reference draws a pixel's samples in sequence from one RNG stream, so sample k starts at
+// draw offset O + sum_{j<k} draws_j, and draws_j depends only on whether camera query j hit:
+// draws_miss (the jitter) or draws_hit (jitter + the direct-lighting samplers, a per-scene
+// constant at depth <= 1).  A group therefore speculates each lane's offset from a hit/miss
+// hypothesis, runs the camera queries, recomputes the offsets from the actual hits, and re-runs
+// exactly the lanes whose offset was wrong, until every offset is the one the sequential order
+// gives (each round fixes at least the first wrong lane).  Shading then runs in parallel, and the
+// group leader folds the samples into the pixel sums in sample order (the reference's float /
+// double accumulation order) with the adaptive stop test at every samples_per_batch boundary;
+// samples past the stop are discarded with their draws.  Results equal the sequential loop's.
+template <bool LEAN, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
+  using namespace rrt;
+  __shared__ ColdLds cl;
+  __shared__ float fr[256], fg[256], fb[256];
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & 63u;
+  const uint32_t G = kp.group;
+  const uint32_t gl = lane & (G - 1u);
+  const uint32_t gbase = lane - gl;
+  const uint64_t gmask = ((G >= 64u) ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+  const uint64_t ltmask = gmask & ((1ull << lane) - 1ull);
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit;
+  const DCamera& cam = kp.cam;
+  Counters cn = {};
+
+  bool have = false, done = false, hyp = false;
+  uint32_t px = 0, py = 0, slot = 0, O = 0;
+  int i = 0;
+  uint64_t key = 0;
+  spec ret = S(0, 0, 0);  // group leader only
+  double s1 = 0.0, s2 = 0.0;
+
+  for (;;) {
+    // ---- claim a pixel (one atomic per group)
+    if (!have && !done) {
+      uint32_t p = 0;
+      if (gl == 0) p = atomicAdd(kp.block_counter, 1u);
+      p = __shfl(p, (int)gbase);
+      if (p >= kp.n_pixels) {
+        done = true;
+      } else {
+        const uint32_t tl = p / tpix, r = p % tpix, lx = r % ts, ly = r / ts;
+        const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
+        if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
+          px = x; py = y; slot = p; key = rrt_pixel_key(kp.seed, x, y);
+          O = 0; i = 0; hyp = false; ret = S(0, 0, 0); s1 = 0.0; s2 = 0.0;
+          have = true;
+        }
+      }
+    }
+    if (__ballot(!done) == 0) break;
+
+    // ---- camera queries at speculated draw offsets, re-run until the offsets are consistent
+    const int left = (int)kp.ns_aa - i;
+    const bool act = have && (int)gl < left;
+    bool valid = false, hit = false, h = hyp;
+    uint32_t off = 0;
+    Isect is;
+    for (;;) {
+      const bool need = act && !valid;
+      if (__ballot(need) == 0) break;
+      const uint32_t nh = (uint32_t)__popcll(__ballot(act && h) & ltmask);
+      if (need) {
+        off = O + nh * Dh + (gl - nh) * Dm;
+        Rng g; g.key = key; g.ctr = off;
+        double jx, jy; g.grid(jx, jy);
+        const double sx = (double)px + jx, sy = (double)py + jy;
+        const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;  // Camera::generate_ray (:182-187)
+        const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+        const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+        hit = query<false, false>(kp, ld3(cam.pos), unit(w), &is, cn);
+      }
+      const uint32_t na = (uint32_t)__popcll(__ballot(act && hit) & ltmask);
+      valid = act && (O + na * Dh + (gl - na) * Dm == off);
+      h = hit;
+    }
+    const uint64_t hits = __ballot(act && hit);
+
+    // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
+    spec s = S(0, 0, 0);
+    if (act && hit) {
+      Rng g; g.key = key; g.ctr = off + Dm;
+      const spec e = emission(kp.bsdfs[is.bsdf]);
+      if (kp.max_ray_depth == 0) s = e;
+      else if (LEAN) s = e + direct_importance_lds<false, true>(kp, g, is, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<false>(kp, g, is, cl, t, cn);
+      else s = e + direct_importance_lds<false, false>(kp, g, is, cl, t, cn);
+    }
+    if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- ordered fold by the group leader (raytrace_pixel's loop body, :136-158)
+    uint32_t stop = 0;
+    if (have && gl == 0) {
+      const int n = left < (int)G ? left : (int)G;
+      for (int k = 0; k < n; ++k) {
+        const spec sk = S(lget(fr, t + k), lget(fg, t + k), lget(fb, t + k));
+        ret = ret + sk;
+        const double il = illum(sk);
+        s1 += il;
+        s2 += il * il;
+        ++i;
+        const bool hk = (hits >> (gbase + k)) & 1ull;
+        O += hk ? Dh : Dm;
+        hyp = hk;
+        bool st = i >= (int)kp.ns_aa;
+        if ((uint32_t)i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
+          const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
+          if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
+        }
+        if (st) { stop = 1; break; }
+      }
+      if (stop) {
+        const spec r = ret / (float)i;
+        kp.rgb[3 * slot] = r.r; kp.rgb[3 * slot + 1] = r.g; kp.rgb[3 * slot + 2] = r.b;
+        kp.count[slot] = i;
+        if (kp.draws) kp.draws[slot] = O;
+      }
+    }
+    stop = __shfl(stop, (int)gbase);
+    i = __shfl(i, (int)gbase);
+    O = __shfl(O, (int)gbase);
+    hyp = __shfl((uint32_t)hyp, (int)gbase) != 0;
+    if (stop) have = false;
+  }
+}
+
+hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
+#define RRT_LAUNCH_B(L, W) hipLaunchKernelGGL((rrt_batch_kernel<L, W>), dim3(grid), dim3(256), 0, stream, kp)
+  if (lean) {
+    switch (waves) {
+      case 2: RRT_LAUNCH_B(true, 2); break;
+      case 4: RRT_LAUNCH_B(true, 4); break;
+      default: RRT_LAUNCH_B(true, 3); break;
+    }
+  } else {
+    RRT_LAUNCH_B(false, 2);
+  }
+#undef RRT_LAUNCH_B
+  return hipGetLastError();
 }
 
 hipError_t rrt_launch_sample(const KParams& kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream) {

@@ -18,11 +18,12 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librrt.so")
+LIB_PATH = os.environ.get("RRT_LIB") or os.path.join(HERE, "librrt.so")  # RRT_LIB: A/B of builds
 
 RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
 RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DIV = 1, 2, 4, 8
-RRT_RENDER_PIXEL_LOOP = 16
+RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_PIXEL = 16, 32, 64, 128
+RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 
 class RRTError(RuntimeError):
@@ -32,7 +33,7 @@ class RRTError(RuntimeError):
 
 
 class DeviceCfg(C.Structure):
-    _fields_ = [("device", C.c_int), ("reserved", C.c_uint32 * 7)]
+    _fields_ = [("device", C.c_int), ("free_grid_res", C.c_uint32), ("reserved", C.c_uint32 * 6)]
 
 
 class CameraDesc(C.Structure):
@@ -55,14 +56,16 @@ class RenderParams(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("n_prims", C.c_uint32), ("n_nodes", C.c_uint32), ("n_leaf_refs", C.c_uint32),
-                ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("last_kernel_ms", C.c_float),
-                ("grid_blocks", C.c_uint32), ("block_threads", C.c_uint32)]
+                ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("grid_n", C.c_uint32 * 3),
+                ("n_clean", C.c_uint32), ("n_big", C.c_uint32),
+                ("grid_free_frac", C.c_float), ("last_kernel_ms", C.c_float), ("grid_blocks", C.c_uint32),
+                ("block_threads", C.c_uint32)]
 
 
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)
 EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
            "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
-           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_bvh",
+           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree",
            "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load"]
 
 _lib = None
@@ -93,6 +96,9 @@ def lib():
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
+        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5)):
+            if hasattr(L, name):  # absent from older builds loaded through RRT_LIB
+                getattr(L, name).argtypes = [vp] * n_args
         L.rrt_scene_file_load.argtypes = [C.c_char_p, C.POINTER(vp)]
         L.rrt_scene_file_desc.restype = vp
         L.rrt_scene_file_desc.argtypes = [vp]
@@ -120,8 +126,8 @@ class SceneFile:
         return lib().rrt_scene_file_desc(self.h)
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rrt_scene_file_free(self.h)
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rrt_scene_file_free(self.h)
             self.h = None
 
 
@@ -155,9 +161,10 @@ def partition_tiles(frame_w, frame_h, tile_size, rank, world):
 class Renderer:
     """One rendering context on one HIP device (device=-1: host-only, for BVH/host tests)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, free_grid_res=0):
         cfg = DeviceCfg()
         cfg.device = device
+        cfg.free_grid_res = free_grid_res
         h = C.c_void_p()
         rc = lib().rrt_create(C.byref(h), C.byref(cfg))
         if rc != RRT_OK:
@@ -166,8 +173,8 @@ class Renderer:
         self.device = device
 
     def close(self):
-        if getattr(self, "h", None):
-            lib().rrt_destroy(self.h)
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rrt_destroy(self.h)
             self.h = None
 
     __del__ = close
@@ -215,6 +222,32 @@ class Renderer:
         s = Stats()
         self._chk(lib().rrt_get_stats(self.h, C.byref(s)))
         return s
+
+    def free_grid(self):
+        """(k [nz][ny][nx] uint8, g0 (3,), inv_h, h_free) of the empty-space grid, or None."""
+        n = np.zeros(3, np.int32)
+        cells = lib().rrt_get_free_grid(self.h, None, None, _p(n))
+        if cells < 0:
+            raise RRTError(cells, "no scene")
+        if cells == 0:
+            return None
+        k = np.zeros((n[2], n[1], n[0]), np.uint8)
+        geom = np.zeros(5, np.float64)
+        self._chk(0 if lib().rrt_get_free_grid(self.h, _p(k), _p(geom), _p(n)) > 0 else RRT_E_INVALID)
+        return k, geom[:3].copy(), float(geom[3]), float(geom[4])
+
+    def clean_tree(self):
+        """(boxes [n,6], nodes [n,4] (skip, first, count, ordinal), big_boxes [nb,6], big [nb,3]
+        (first, count, ordinal)) of the clean tree, or None."""
+        s = self.stats()
+        if s.n_clean == 0:
+            return None
+        boxes = np.zeros((s.n_clean, 6), np.float64)
+        nodes = np.zeros((s.n_clean, 4), np.int32)
+        bb = np.zeros((max(s.n_big, 1), 6), np.float64)
+        big = np.zeros((max(s.n_big, 1), 3), np.int32)
+        self._chk(0 if lib().rrt_get_clean_tree(self.h, _p(boxes), _p(nodes), _p(bb), _p(big)) > 0 else RRT_E_INVALID)
+        return boxes, nodes, bb[:s.n_big], big[:s.n_big]
 
     def bvh(self):
         s = self.stats()

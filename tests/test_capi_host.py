@@ -99,3 +99,131 @@ def test_errors(host_ctx):
     st = rrt.SpacetimeDesc()
     st.delta_theta = 0.0
     assert rrt.lib().rrt_set_spacetime(host_ctx.h, C.byref(st)) == rrt.RRT_E_INVALID
+
+
+def _seg_dist(p, a, b):
+    ab = b - a
+    t = np.clip(((p - a) * ab).sum(-1) / np.maximum((ab * ab).sum(-1), 1e-300), 0.0, 1.0)
+    d = p - (a + t[..., None] * ab)
+    return np.sqrt((d * d).sum(-1))
+
+
+def _tri_dist(p, a, b, c):
+    """Euclidean distance from points p [m,1,3] to triangles a, b, c [1,t,3] -> [m,t]."""
+    n = np.cross(b - a, c - a)
+    nn = np.maximum((n * n).sum(-1), 1e-300)
+    w = p - a
+    h = (w * n).sum(-1) / nn
+    q = p - h[..., None] * n                     # projection onto the plane
+    def side(u, v):
+        return (np.cross(v - u, q - u) * n).sum(-1)
+    inside = (side(a, b) >= 0) & (side(b, c) >= 0) & (side(c, a) >= 0)
+    d_in = np.abs(h) * np.sqrt(nn)
+    d_edge = np.minimum(np.minimum(_seg_dist(p, a, b), _seg_dist(p, b, c)), _seg_dist(p, c, a))
+    return np.where(inside, d_in, d_edge)
+
+
+def _scene_prims(path):
+    """Triangles (a, b, c) and spheres (centre, r) of a .rrts file (include/rrt_scene_format.h)."""
+    raw = open(path, "rb").read()
+    nb, no, _, _ = np.frombuffer(raw, "<u4", 4, 8)
+    off = 24 + 64 * int(nb)
+    tris, sph = [], []
+    for _ in range(int(no)):
+        kind, _, a, b = np.frombuffer(raw, "<u4", 4, off)
+        off += 16
+        if kind == 0:
+            pos = np.frombuffer(raw, "<f8", 3 * int(a), off).reshape(-1, 3)
+            off += 48 * int(a)
+            idx = np.frombuffer(raw, "<u4", 3 * int(b), off).reshape(-1, 3)
+            off += 12 * int(b)
+            tris.append(pos[idx])
+        else:
+            v = np.frombuffer(raw, "<f8", 4, off)
+            off += 32
+            sph.append(v)
+    return (np.concatenate(tris) if tris else np.zeros((0, 3, 3))), np.array(sph).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("scene", ["CBbunny", "CBspheres_lambertian", "CBcoil", "CBgems"])
+def test_free_grid_is_conservative(host_ctx, scene):
+    """Empty-space grid: from any point p, the free radius (k - 2) * h_free that
+    the kernel reads for p's cell never exceeds p's true distance to the nearest primitive, and
+    (for the floating-point hit region of Triangle::intersect) to the nearest triangle plane
+    inside that triangle's leaf box -- so a skipped micro segment meets no primitive test that
+    could accept it, and skipping it is result-identical.  The GPU parity tests check the
+    rendered frames bit for bit with and without the grid."""
+    path = os.path.join(GOLD, "scenes", scene + ".rrts")
+    host_ctx.set_scene(rrt.SceneFile(path))
+    g = host_ctx.free_grid()
+    assert g is not None
+    k, g0, inv_h, h_free = g
+    tris, sph = _scene_prims(path)
+    rng = np.random.default_rng(7)
+    n = np.array(k.shape[::-1])
+    span = n / inv_h
+    pts = g0 + rng.uniform(-0.02, 1.02, size=(600, 3)) * span
+    if len(tris):  # points hugging primitives, where the bound is tight
+        t = tris[rng.integers(0, len(tris), 600)]
+        wts = rng.dirichlet([1, 1, 1], 600)
+        pts = np.concatenate([pts, (wts[:, :, None] * t).sum(1) + rng.normal(0, 4 / inv_h, (600, 3))])
+    f = (pts - g0) * inv_h                       # same arithmetic as segment_clear()
+    inside = np.all((f >= 0) & (f < n), axis=1)
+    pts, f = pts[inside], f[inside]
+    idx = f.astype(np.int64)
+    free = (k[idx[:, 2], idx[:, 1], idx[:, 0]].astype(np.float64) - 2) * h_free
+    assert (free > 0).mean() > 0.2
+    dist = np.full(len(pts), np.inf)
+    for i in range(0, len(pts), 64):
+        p = pts[i:i + 64, None, :]
+        if len(tris):
+            dist[i:i + 64] = _tri_dist(p, tris[None, :, 0], tris[None, :, 1], tris[None, :, 2]).min(1)
+        if len(sph):
+            ds = np.sqrt(((p - sph[None, :, :3]) ** 2).sum(-1)) - sph[None, :, 3]
+            dist[i:i + 64] = np.minimum(dist[i:i + 64], np.maximum(ds, 0).min(1))
+    assert (dist - free).min() >= 0.0, (dist - free).min()
+    s = host_ctx.stats()
+    assert list(s.grid_n) == list(n) and 0.0 < s.grid_free_frac < 1.0
+
+
+@pytest.mark.parametrize("scene", ["CBbunny", "CBcoil", "CBgems"])
+def test_clean_walk_matches_reference_walk(host_ctx, scene):
+    """The clean-tree walk (oversized leaves listed apart, inner boxes refit), with and without the
+    plane cull in front of primitive tests, returns the same closest hit (leaf slot and t, bit for
+    bit) as the reference walk, on segments aimed at primitives, grazing them, inside the room
+    and far outside."""
+    from walk_sim import Walker
+    path = os.path.join(GOLD, "scenes", scene + ".rrts")
+    host_ctx.set_scene(rrt.SceneFile(path))
+    ct = host_ctx.clean_tree()
+    assert ct is not None and len(ct[3]) > 0
+    boxes, nodes, prims = host_ctx.bvh()
+    tris, _ = _scene_prims(path)
+    t = tris[prims.astype(np.int64)]
+    geo = np.concatenate([t[:, 0], t[:, 1] - t[:, 0], t[:, 2] - t[:, 0]], 1)
+    w = Walker(boxes, nodes, geo, ct)
+    w.planes(1e-9 * max(1.0, float(np.abs(boxes[0]).max())))
+    rng = np.random.default_rng(3)
+    lo, hi = boxes[0, :3], boxes[0, 3:]
+    n_hit = 0
+    for i in range(400):
+        if i % 4 == 0:    # far away, long
+            o = lo + rng.uniform(-2, 3, 3) * (hi - lo)
+            L = rng.uniform(0.1, 20)
+        else:             # near a primitive, short, often grazing
+            k = rng.integers(len(t))
+            tgt = rng.dirichlet([1, 1, 1]) @ t[k]
+            o = tgt + rng.normal(0, 0.05, 3)
+            L = rng.uniform(0.01, 0.3)
+        dv = rng.normal(size=3)
+        if i % 7 == 0:
+            dv[rng.integers(3)] = 0.0  # axis-parallel component
+        d = dv / np.linalg.norm(dv)
+        o, d = tuple(float(v) for v in o), tuple(float(v) for v in d)
+        ref = w.reference(o, d, float(L))
+        got = w.clean(o, d, float(L))
+        assert ref[:2] == got[:2], (i, ref, got)
+        got = w.clean(o, d, float(L), cull=True)
+        assert ref[:2] == got[:2], (i, ref, got)
+        n_hit += ref[0] >= 0
+    assert n_hit > 20

@@ -23,7 +23,7 @@ def gpu():
     r.close()
 
 
-def render(gpu, c, draws=True, counters=False):
+def render(gpu, c, draws=True, counters=False, flags=0):
     gpu.set_scene(rrt.SceneFile(c.scene_path))
     gpu.set_camera(rrt.load_camera(c.camera_path))
     bh = c.cfg["bh"]
@@ -31,7 +31,7 @@ def render(gpu, c, draws=True, counters=False):
     g = c.cfg
     p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
                           ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
-                          max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"])
+                          max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=flags)
     return gpu.render(p, c.x0, c.y0, c.w, c.h, draws=draws, counters=counters)
 
 
@@ -49,10 +49,20 @@ def check(c, rgb, cnt, draws):
     return m
 
 
+# every kernel path must meet the same bar: default (sample-parallel kernel, clean-tree BVH walk,
+# empty-space grid), the reference-tree walk without the grid, the lane-per-pixel per-sample
+# kernel, the per-pixel-loop kernel and the wavefront state-machine kernel
+VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
+            "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
+            "wavefront": rrt.RRT_RENDER_WAVEFRONT}
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("name", SMALL)
-def test_small_cases(gpu, name):
+def test_small_cases(gpu, name, variant):
     c = Case(name)
-    rgb, cnt, draws, _ = render(gpu, c)
+    rgb, cnt, draws, _ = render(gpu, c, flags=VARIANTS[variant])
+    print(variant, end=" ")
     check(c, rgb, cnt, draws)
 
 

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase wave time of the depth<=1 per-sample kernel, from a build with
+-DRRT_PROFILE=1 (make -C relativistic-ray-tracer_amd EXTRA=-DRRT_PROFILE=1), loaded through
+RRT_LIB.  Prints the share of wave time spent in the geodesic queries, their micro steps and
+their BVH walks (busiest lane per wave, summed over waves)."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import torch  # noqa: E402,F401
+import rrt  # noqa: E402
+from golden_cases import Case  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="cfg3_bunny_1080p_s64")
+    ap.add_argument("--flags", type=int, nargs="+", default=[0, rrt.RRT_RENDER_NO_CLEAN])
+    a = ap.parse_args()
+    c = Case(a.case)
+    g = c.cfg
+    L = rrt.lib()
+    L.rrt_prof_read.argtypes = [C.c_void_p]
+    r = rrt.Renderer(0)
+    r.set_scene(rrt.SceneFile(c.scene_path))
+    r.set_camera(rrt.load_camera(c.camera_path))
+    r.set_black_hole(g["bh"][:3], g["bh"][3], g["bh"][4])
+    tiles = rrt.partition_tiles(c.frame_w, c.frame_h, 32, 0, 1)
+    n = len(tiles) * 1024
+    prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
+    pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    buf = np.zeros(8 + 3 * 16384, np.uint64)
+    out = {}
+    for fl in a.flags:
+        p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                              ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                              max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=fl)
+        L.rrt_prof_read(buf.ctypes.data)
+        r.render_tiles_device(p, tiles, 32, prgb.data_ptr(), pcnt.data_ptr())
+        ms = r.stats().last_kernel_ms
+        L.rrt_prof_read(buf.ctypes.data)
+        tot, tq, tm, tt = (float(v) for v in buf[:4])
+        t0, t1, nw, tex = int(buf[4]), int(buf[5]), int(buf[6]), int(buf[7])
+        span = t1 - t0
+        m = min(nw, 16384)
+        ends = (buf[8:8 + m].astype(np.float64) - t0) / span
+        starts = (buf[8 + 16384:8 + 16384 + m].astype(np.float64) - t0) / span
+        work = buf[8 + 2 * 16384:8 + 2 * 16384 + m]
+        blocks, samples = (work >> np.uint64(32)).astype(np.int64), (work & np.uint64(0xffffffff)).astype(np.int64)
+        res = blocks > 0
+        np.savez(f"gpurun_out/waves_{fl}.npz", ends=ends, starts=starts, blocks=blocks, samples=samples)
+        out[fl] = {"kernel_ms": ms, "ticks_per_ms": span / ms, "waves": nw, "waves_with_work": int(res.sum()),
+                   "exhausted_at": (tex - t0) / span, "wave_cycles": tot,
+                   "query": tq / tot, "micro": tm / tot, "walk": tt / tot,
+                   "other_in_query": (tq - tm - tt) / tot, "outside_query": 1 - tq / tot,
+                   "busy_frac_working_waves": float(((ends - starts)[res]).sum() / max(res.sum(), 1)),
+                   "working_wave_end_q": [round(float(q), 3) for q in np.quantile(ends[res], [0.05, 0.25, 0.5, 0.75, 0.95, 1.0])],
+                   "working_wave_start_q": [round(float(q), 3) for q in np.quantile(starts[res], [0.05, 0.5, 0.95, 1.0])]}
+    print(json.dumps({"case": a.case, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
