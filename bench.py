@@ -45,6 +45,7 @@ WORKLOADS = {
 TILE = 32
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic bytes
+BYTES_PLANE = 32  # plane-cull record (DPlane) read per plane test
 
 
 def cpu_baseline(wl, threads, row_stride):
@@ -78,6 +79,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-row-stride", type=int, default=8)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+                    help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic")
     a = ap.parse_args()
 
     import torch
@@ -154,23 +157,37 @@ def main():
     elapsed = float(elapsed.item())
     k_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kern_ms]))
 
-    # algorithmic work of this rank's launch: counting variant, outside the timed region
+    kernel_name = r.stats().kernel.decode()
+
+    # work of this rank's launch, counted by the counting kernel outside the timed region: the
+    # work the renderer executes (roofline) and the reference algorithm's work
     n_loc = len(tiles)
-    ctr = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
-    cparams = rrt.render_params(W, H, ns_aa=wl["spp"], flags=rrt.RRT_RENDER_COUNTERS)
-    tmp = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
-    r.render_tiles_device(cparams, tiles, TILE, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
-                          d_counters=ctr.data_ptr(), stream=s_handle)
-    torch.cuda.synchronize()
-    c4 = ctr.view(-1, 4).to(torch.int64).sum(0).cpu().numpy()
-    cnt_local = tmp[n_loc * tpix * 3:n_loc * tpix * 4].to(torch.int64).sum()
     pix_local = sum(min(TILE, W - int(x)) * min(TILE, H - int(y)) for x, y in tiles)
-    stats = torch.tensor([float(cnt_local), float(c4[0]), float(c4[1]), float(c4[2]), float(c4[3]), float(pix_local)],
-                         dtype=torch.float64, device=dev)
-    loc_bytes = BYTES_AABB * c4[0] + BYTES_PRIM * c4[2] + BYTES_PIXEL * pix_local
-    if world > 1:
-        dist.all_reduce(stats)
-    samples, bbox, micro, prim, queries, pixels = [float(v) for v in stats.cpu().numpy()]
+
+    def count_pass(flags):
+        ctr = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
+        tmp = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
+        cparams = rrt.render_params(W, H, ns_aa=wl["spp"], flags=rrt.RRT_RENDER_COUNTERS | flags)
+        r.render_tiles_device(cparams, tiles, TILE, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
+                              d_counters=ctr.data_ptr(), stream=s_handle)
+        torch.cuda.synchronize()
+        c4 = ctr.view(-1, 4).to(torch.int64).sum(0).cpu().numpy()
+        cnt = float(tmp[n_loc * tpix * 3:n_loc * tpix * 4].to(torch.int64).sum().item())
+        t = torch.tensor([cnt] + [float(v) for v in c4] + [float(pix_local)], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t)
+        return [float(v) for v in t.cpu().numpy()], c4
+
+    (samples, bbox, micro, prim, queries, pixels), _ = count_pass(0)
+    (_, x_bbox, x_micro, x_prim, x_plane, _), xc4 = count_pass(rrt.RRT_RENDER_COUNT_EXECUTED)
+    loc_bytes = BYTES_AABB * xc4[0] + BYTES_PRIM * xc4[2] + BYTES_PLANE * xc4[3] + BYTES_PIXEL * pix_local
+    ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
+    traffic = None
+    if a.traffic and os.path.exists(a.traffic):
+        with open(a.traffic) as f:
+            tr = json.load(f)
+        if tr.get("workload") == a.workload and tr.get("kernel") == kernel_name:
+            traffic = tr["hbm_bytes_per_launch"]
 
     if rank == 0:
         # sanity: the gathered frame holds every pixel's sample count
@@ -178,6 +195,10 @@ def main():
         assert frame_samples == int(samples), (frame_samples, samples)
         value = samples * a.steps / elapsed / 1e6
         achieved = loc_bytes / (k_ms * 1e-3) / 1e9
+        work = {"aabb_tests": bbox / samples, "micro_steps": micro / samples, "prim_tests": prim / samples,
+                "queries": queries / samples}
+        xwork = {"aabb_tests": x_bbox / samples, "micro_steps": x_micro / samples, "prim_tests": x_prim / samples,
+                 "plane_tests": x_plane / samples}
         out = {
             "metric": "Msamples/sec (whole node), 1080p 64spp CBbunny + Schwarzschild geodesic"
             if a.workload == "cfg3" else f"Msamples/sec (whole node), {wl['desc']}",
@@ -197,12 +218,14 @@ def main():
             "samples_per_frame": int(samples),
             "nominal_msamples_per_s": W * H * wl["spp"] * a.steps / elapsed / 1e6,
             "kernel_ms_rank0": k_ms,
-            "work_per_sample": {"aabb_tests": bbox / samples, "micro_steps": micro / samples,
-                                "prim_tests": prim / samples, "queries": queries / samples},
+            "work_per_sample_reference": work,
+            "work_per_sample_executed": xwork,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "rrt_render_kernel<false,false>",
-                         "algorithmic_bytes_per_launch": float(loc_bytes)},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": kernel_name,
+                         "algorithmic_bytes_per_launch": float(loc_bytes),
+                         "reference_algorithm_bytes_per_launch": float(ref_bytes),
+                         "reference_equivalent_GBps": ref_bytes / (k_ms * 1e-3) / 1e9},
         }
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))

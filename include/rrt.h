@@ -145,6 +145,10 @@ enum {
                                      are identical) */
   RRT_RENDER_PER_PIXEL = 1u << 7, /* depth <= 1: one lane per pixel (per-sample kernel) instead
                                      of the sample-parallel kernel (A/B testing) */
+  RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
+                                     (AABB tests incl. oversized leaves, primitive tests after
+                                     the plane cull, micro steps, and plane tests in place of
+                                     queries) instead of the reference's */
   /* diagnostics only -- results are NOT the reference's: */
   RRT_RENDER_DIAG_NO_INTERIOR = 1u << 28, /* skip walks of segments starting in the root box */
   RRT_RENDER_DIAG_NO_EXTERIOR = 1u << 29, /* skip walks of segments starting outside it */
@@ -196,6 +200,7 @@ typedef struct {
   float grid_free_frac;       /* fraction of grid cells with free radius > 0 */
   float last_kernel_ms;       /* HIP-event time of the last render launch */
   uint32_t grid_blocks, block_threads;
+  char kernel[48];            /* name of the last render kernel launched */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 /* Host copy of the flattened BVH: boxes [n][6] (min, max), nodes [n][4] (first, count, left,

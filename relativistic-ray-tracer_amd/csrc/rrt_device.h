@@ -205,6 +205,16 @@ __device__ __forceinline__ bool segment_clear(const DGrid& g, v3 o, double max_t
   const int k = (int)g.k[(iz * g.n[1] + iy) * g.n[0] + ix];
   return (double)(k - 2) * g.h_free > max_t;
 }
+// Does the segment [o, e] keep, along some axis, more than plane_eps (~1e6 ulps of the scene
+// scale) outside the root box?  Then the reference's first test -- the root box slab test --
+// fails: on that axis both quotients (bound - o) / d have the sign and size of a point outside
+// [0, max_t] by far more than rounding (d = 0: both are the same infinity), so tmin > max_t or
+// tmax < 0.  Nothing else of the walk runs, so skipping it (and the reciprocals it needs) is
+// result-identical.
+__device__ __forceinline__ bool segment_outside_root(const KParams& kp, v3 o, v3 e) {
+  return fmax(o.x, e.x) < kp.root_lo[0] || fmin(o.x, e.x) > kp.root_hi[0] || fmax(o.y, e.y) < kp.root_lo[1] ||
+         fmin(o.y, e.y) > kp.root_hi[1] || fmax(o.z, e.z) < kp.root_lo[2] || fmin(o.z, e.z) > kp.root_hi[2];
+}
 // Sphere::test + the range checks of Sphere::intersect (sphere.cpp:10-53), min_t = 0
 __device__ __forceinline__ bool sphere_t(v3 c, double r2, v3 o, v3 d, double max_t, double& t) {
   v3 tmp = o - c;
@@ -292,13 +302,16 @@ __device__ __forceinline__ bool plane_may_hit(const DPlane& pl, v3 o, v3 e, doub
 }
 // leaf_prims with the plane cull in front of every primitive test (skipped primitives are ones
 // the reference tests and rejects, so the answer is the same)
-template <bool ANY>
+template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool leaf_prims_cull(const KParams& kp, int first, int count, v3 o, v3 d, v3 e,
-                                                double& max_t, int& hit_slot, double& hb1, double& hb2) {
+                                                double& max_t, int& hit_slot, double& hb1, double& hb2,
+                                                Counters& cn) {
   bool hit = false;
   for (int i = 0; i < count; ++i) {
     const int slot = first + i;
+    if (COUNT) cn.query++;  // plane tests (executed-work counting)
     if (!plane_may_hit(kp.planes[slot], o, e, kp.plane_eps)) continue;
+    if (COUNT) cn.prim++;
     const DPrimMeta meta = kp.meta[slot];
     const DPrimGeo gp = kp.geo[slot];
     double t, b1 = 0, b2 = 0;
@@ -312,9 +325,11 @@ __device__ __forceinline__ bool leaf_prims_cull(const KParams& kp, int first, in
   return hit;
 }
 // Does any primitive of the leaf survive the plane cull?
-__device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int count, v3 o, v3 e) {
+template <bool COUNT>
+__device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int count, v3 o, v3 e, Counters& cn) {
   bool any = false;
   for (int i = 0; i < count; ++i) any |= plane_may_hit(kp.planes[first + i], o, e, kp.plane_eps);
+  if (COUNT) cn.query += (uint32_t)count;
   return any;
 }
 
@@ -330,9 +345,10 @@ __device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int c
 // is left; the oversized leaves are tested directly from a short list, merged in by their
 // left-first ordinal.  The reference's root test comes first, so rays outside the scene still
 // cost one box test.
-template <bool ANY, bool EXACT>
+template <bool ANY, bool EXACT, bool COUNT>
 __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
-                                               double& hb1, double& hb2) {
+                                               double& hb1, double& hb2, Counters& cn) {
+  if (COUNT) cn.bbox++;
   if (!slab<EXACT>(kp.nodes[0], o, d, y, max_t)) return false;
   const v3 e = o + vmul(d, max_t);  // far end point (cull only; max_t only shrinks below)
   bool hit = false;
@@ -348,8 +364,9 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
     while (next_big < lim) {                    // oversized leaves that come first
       const DBig& bg = kp.big[bi];
       // primitives first: an oversized leaf's box (the room) passes for almost every segment
-      if (leaf_may_hit(kp, bg.first, bg.count, o, e) && slab<EXACT>(bg.mn, bg.mx, o, d, y, max_t) &&
-          leaf_prims_cull<ANY>(kp, bg.first, bg.count, o, d, e, max_t, hit_slot, hb1, hb2)) {
+      if (leaf_may_hit<COUNT>(kp, bg.first, bg.count, o, e, cn) && (COUNT ? (cn.bbox++, true) : true) &&
+          slab<EXACT>(bg.mn, bg.mx, o, d, y, max_t) &&
+          leaf_prims_cull<ANY, COUNT>(kp, bg.first, bg.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
         hit = true;
         if (ANY) return true;
       }
@@ -357,9 +374,10 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
       next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
     }
     if (!more) break;
+    if (COUNT) cn.bbox++;
     if (!slab<EXACT>(n, o, d, y, max_t)) { node = n.skip; continue; }
     if (n.count == 0) { node = node + 1; continue; }
-    if (leaf_prims_cull<ANY>(kp, n.first, n.count, o, d, e, max_t, hit_slot, hb1, hb2)) {
+    if (leaf_prims_cull<ANY, COUNT>(kp, n.first, n.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
       hit = true;
       if (ANY) return true;
     }
@@ -400,7 +418,10 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
 // ignored, as in the reference).  Capture by the hole returns "no hit".
 template <bool ANY, bool COUNT>
 __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  if (COUNT && !(kp.diag & 2)) cn.query++;
+  // COUNT && kp.count_exec: count the work this path executes (grid / root skips, clean walk,
+  // plane tests in the query slot) instead of the reference's
+  const bool opt = !COUNT || kp.count_exec;
+  if (COUNT && !kp.count_exec && !(kp.diag & 2)) cn.query++;
   RRT_T0(tq0);
   double max_t = 0.0;
   const v3 hc = V(kp.hole.c[0], kp.hole.c[1], kp.hole.c[2]);
@@ -414,7 +435,8 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
       RRT_ACC(t_query, tq0);
       return false;
     }
-    if (!COUNT && segment_clear(kp.grid, o, max_t)) continue;  // no primitive within reach
+    if (opt && segment_outside_root(kp, o, o + vmul(d, max_t))) continue;  // root test fails
+    if (opt && segment_clear(kp.grid, o, max_t)) continue;  // no primitive within reach
     if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
       const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
                       o.y <= kp.nodes[0].mx[1] && o.z >= kp.nodes[0].mn[2] && o.z <= kp.nodes[0].mx[2];
@@ -432,9 +454,9 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
     const bool fast = segment_fast(kp, o, d);
     RRT_T0(tt0);
     bool hit;
-    if (!COUNT && kp.clean_nodes)
-      hit = fast ? traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2)
-                 : traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2);
+    if (opt && kp.clean_nodes)
+      hit = fast ? traverse_clean<ANY, false, COUNT>(kp, o, d, y, seg_t, slot, b1, b2, cn)
+                 : traverse_clean<ANY, true, COUNT>(kp, o, d, y, seg_t, slot, b1, b2, cn);
     else
       hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                  : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);

@@ -124,6 +124,7 @@ struct rrt_ctx {
   float last_ms = 0.f;
   bool timed = false;
   uint32_t last_grid = 0;
+  std::string last_kernel;
 };
 
 static int fail(rrt_ctx* c, int code, const std::string& msg) {
@@ -682,10 +683,20 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.clean_nodes = use_clean ? c->d_clean : nullptr;
   kp.big = c->d_big; kp.clean_root = c->clean_root; kp.n_big = c->n_big;
   kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
+  {
+    const Box& rb = c->nodes[0].bb;
+    const double lo[3] = {rb.mn.x, rb.mn.y, rb.mn.z}, hi[3] = {rb.mx.x, rb.mx.y, rb.mx.z};
+    const bool ok = c->plane_eps > 0 && !(p->flags & RRT_RENDER_NO_SKIP);
+    for (int k = 0; k < 3; ++k) {  // no skip: an empty test range (-inf, +inf)
+      kp.root_lo[k] = ok ? lo[k] - c->plane_eps : -INFINITY;
+      kp.root_hi[k] = ok ? hi[k] + c->plane_eps : INFINITY;
+    }
+  }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
   kp.direct_hemisphere = p->direct_hemisphere; kp.seed = p->seed;
   kp.diag = (p->flags >> 30) | ((p->flags >> 26) & 12u);
+  kp.count_exec = (p->flags & RRT_RENDER_COUNT_EXECUTED) ? 1u : 0u;
   kp.frame_w = (double)p->frame_w; kp.frame_h = (double)p->frame_h;
   kp.frame_wi = p->frame_w; kp.frame_hi = p->frame_h;
   kp.tiles = c->d_tiles; kp.n_tiles = n_tiles; kp.tile_size = ts;
@@ -738,14 +749,23 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (grid == 0) grid = 1;
   c->last_grid = grid;
   HIPCHK(c, hipEventRecord(c->ev0, stream));
-  if (batch)
+  const char* tf[2] = {"false", "true"};
+  char name[64];
+  if (batch) {
+    const int w = lean ? (waves == 2 || waves == 4 ? waves : 3) : 2;
+    std::snprintf(name, sizeof(name), "rrt_batch_kernel<%s, %d>", tf[lean], w);
     HIPCHK(c, rrt_launch_batch(kp, lean, waves, grid, stream));
-  else if (mega)
+  } else if (mega) {
+    std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
     HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
-  else if (pixel_loop)
+  } else if (pixel_loop) {
+    std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %s, ...>", tf[deep], tf[count], tf[lean]);
     HIPCHK(c, rrt_launch_render(kp, deep, count, lean, waves, grid, stream));
-  else
+  } else {
+    std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %s, ...>", tf[count], tf[lean]);
     HIPCHK(c, rrt_launch_sample(kp, count, lean, waves, grid, stream));
+  }
+  c->last_kernel = name;
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
   return RRT_OK;
@@ -851,6 +871,7 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
   out->max_depth = c->max_depth;
   out->device_bytes = c->device_bytes;
   out->grid_blocks = c->last_grid;
+  std::snprintf(out->kernel, sizeof(out->kernel), "%s", c->last_kernel.c_str());
   out->n_clean = c->has_clean ? (uint32_t)c->clean.size() : 0u;
   out->n_big = c->has_clean ? (uint32_t)c->big.size() : 0u;
   if (!c->grid.empty()) {

@@ -92,6 +92,7 @@ struct KParams {
   DGrid grid;
   const DNode* clean_nodes;   // clean tree (pad = first leaf ordinal); null: reference walk only
   const DPlane* planes;       // per leaf slot; null: no plane cull
+  double root_lo[3], root_hi[3];  // root box widened by plane_eps (segment_outside_root)
   double plane_eps;           // plane-cull margin (scene-scaled, ~1e6 x rounding error)
   const DBig* big;            // oversized leaves by left-first ordinal
   int32_t clean_root;         // 0, or -1 if every leaf is oversized
@@ -103,6 +104,7 @@ struct KParams {
   float max_tolerance;
   uint32_t direct_hemisphere;
   uint32_t diag;  // RRT_RENDER_DIAG_* bits >> 30 (bit 0: no traversal, bit 1: clear-segment stats)
+  uint32_t count_exec;  // with counters: count the executed work (RRT_RENDER_COUNT_EXECUTED)
   uint64_t seed;
   double frame_w, frame_h;
   uint32_t frame_wi, frame_hi;

@@ -284,6 +284,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit;
   const DCamera& cam = kp.cam;
   Counters cn = {};
+#if RRT_PROFILE
+  const uint64_t t_start = clock64(), w_start = wall_clock64();
+  uint32_t prof_blocks = 0, prof_samples = 0;  // pixels claimed, query rounds
+#endif
 
   bool have = false, done = false, hyp = false;
   uint32_t px = 0, py = 0, slot = 0, O = 0;
@@ -300,7 +304,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
       p = __shfl(p, (int)gbase);
       if (p >= kp.n_pixels) {
         done = true;
+#if RRT_PROFILE
+        if (gl == 0) atomicMin(&rrt_prof[7], (unsigned long long)wall_clock64());
+#endif
       } else {
+#if RRT_PROFILE
+        ++prof_blocks;
+#endif
         const uint32_t tl = p / tpix, r = p % tpix, lx = r % ts, ly = r / ts;
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
         if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
@@ -321,6 +331,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
     for (;;) {
       const bool need = act && !valid;
       if (__ballot(need) == 0) break;
+#if RRT_PROFILE
+      ++prof_samples;
+#endif
       const uint32_t nh = (uint32_t)__popcll(__ballot(act && h) & ltmask);
       if (need) {
         off = O + nh * Dh + (gl - nh) * Dm;
@@ -387,6 +400,27 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
     hyp = __shfl((uint32_t)hyp, (int)gbase) != 0;
     if (stop) have = false;
   }
+#if RRT_PROFILE
+  const uint64_t t_end = clock64(), w_end = wall_clock64();
+  uint64_t v[4] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav};
+  for (int k = 0; k < 4; ++k) {
+    for (int off2 = 32; off2 > 0; off2 >>= 1) {
+      const uint64_t o2 = __shfl_xor(v[k], off2);
+      v[k] = v[k] > o2 ? v[k] : o2;
+    }
+    if (lane == 0) atomicAdd(&rrt_prof[k], (unsigned long long)v[k]);
+  }
+  uint32_t nb = gl == 0 ? prof_blocks : 0;
+  for (int off2 = 32; off2 > 0; off2 >>= 1) nb += __shfl_xor(nb, off2);
+  if (lane == 0) {
+    atomicMin(&rrt_prof[4], (unsigned long long)w_start);
+    atomicMax(&rrt_prof[5], (unsigned long long)w_end);
+    const unsigned long long w = atomicAdd(&rrt_prof[6], 1ull) & 16383;
+    rrt_prof_ends[w] = w_end;
+    rrt_prof_starts[w] = w_start;
+    rrt_prof_work[w] = ((unsigned long long)nb << 32) | prof_samples;
+  }
+#endif
 }
 
 hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t grid, hipStream_t stream) {

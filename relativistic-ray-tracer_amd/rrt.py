@@ -23,6 +23,7 @@ LIB_PATH = os.environ.get("RRT_LIB") or os.path.join(HERE, "librrt.so")  # RRT_L
 RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
 RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DIV = 1, 2, 4, 8
 RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_PIXEL = 16, 32, 64, 128
+RRT_RENDER_COUNT_EXECUTED = 256
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 
@@ -59,7 +60,7 @@ class Stats(C.Structure):
                 ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("grid_n", C.c_uint32 * 3),
                 ("n_clean", C.c_uint32), ("n_big", C.c_uint32),
                 ("grid_free_frac", C.c_float), ("last_kernel_ms", C.c_float), ("grid_blocks", C.c_uint32),
-                ("block_threads", C.c_uint32)]
+                ("block_threads", C.c_uint32), ("kernel", C.c_char * 48)]
 
 
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)

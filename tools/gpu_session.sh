@@ -21,7 +21,10 @@ for step in "$@"; do
   case $step in
     test)  run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q -s ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
+    bench) run bench 600 python3 bench.py --steps 5 --warmup 2 --traffic gpurun_out/traffic.json ;;
+    traffic) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
+           run traffic 60 python3 tools/pmc_traffic.py ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}

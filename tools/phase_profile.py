@@ -62,7 +62,8 @@ def main():
                    "other_in_query": (tq - tm - tt) / tot, "outside_query": 1 - tq / tot,
                    "busy_frac_working_waves": float(((ends - starts)[res]).sum() / max(res.sum(), 1)),
                    "working_wave_end_q": [round(float(q), 3) for q in np.quantile(ends[res], [0.05, 0.25, 0.5, 0.75, 0.95, 1.0])],
-                   "working_wave_start_q": [round(float(q), 3) for q in np.quantile(starts[res], [0.05, 0.5, 0.95, 1.0])]}
+                   "working_wave_start_q": [round(float(q), 3) for q in np.quantile(starts[res], [0.05, 0.5, 0.95, 1.0])],
+                   "claims_per_wave": float(blocks[res].mean()), "rounds_per_wave": float(samples[res].mean())}
     print(json.dumps({"case": a.case, "results": out}, indent=1))
 
 
