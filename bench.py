@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
 
 import rrt  # noqa: E402
+import rrt_frame  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
@@ -105,20 +106,18 @@ def main():
     r.set_black_hole(*wl["bh"])
     params = rrt.render_params(W, H, ns_aa=wl["spp"])
 
-    tiles = rrt.partition_tiles(W, H, TILE, rank, world)
-    n_max = len(rrt.partition_tiles(W, H, TILE, 0, world))  # rank 0 holds the most tiles
-    tpix = TILE * TILE
-    # packed per-rank result: [n_max * tpix * 3] f32 rgb, then [n_max * tpix] i32 counts
-    packed = torch.zeros(n_max * tpix * 4, dtype=torch.int32, device=dev)
+    plan = rrt_frame.FramePlan(W, H, world, TILE)
+    tiles = plan.tiles(rank)
+    tpix = plan.tpix
+    # packed per-rank result (rrt_frame.py layout): f32 rgb then i32 counts
+    packed = torch.zeros(plan.words, dtype=torch.int32, device=dev)
     p_rgb = packed.data_ptr()
-    p_cnt = packed.data_ptr() + n_max * tpix * 3 * 4
+    p_cnt = packed.data_ptr() + plan.count_offset * 4
     stream = torch.cuda.current_stream()
     s_handle = stream.cuda_stream
     if rank == 0:
         frame_rgb = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
         frame_cnt = torch.zeros(H * W, dtype=torch.int32, device=dev)
-        gather_bufs = [torch.zeros_like(packed) for _ in range(world)] if world > 1 else [packed]
-        rank_tiles = [rrt.partition_tiles(W, H, TILE, q, world) for q in range(world)]
 
     kern_ms = []
 
@@ -128,12 +127,11 @@ def main():
         e0.record(stream)
         r.render_tiles_device(params, tiles, TILE, p_rgb, p_cnt, stream=s_handle)
         e1.record(stream)
-        if world > 1:
-            dist.gather(packed, gather_bufs if rank == 0 else None, dst=0)
+        bufs = rrt_frame.gather(dist, packed, rank, world)  # RCCL over xGMI; the only exchange
         if rank == 0:
             for q in range(world):
-                base = gather_bufs[q].data_ptr()
-                r.unpack_tiles_device(rank_tiles[q], TILE, W, H, base, base + n_max * tpix * 3 * 4,
+                base = bufs[q].data_ptr()
+                r.unpack_tiles_device(plan.tiles(q), TILE, W, H, base, base + plan.count_offset * 4,
                                       frame_rgb.data_ptr(), frame_cnt.data_ptr(), stream=s_handle)
         if timed:
             kern_ms.append((e0, e1))

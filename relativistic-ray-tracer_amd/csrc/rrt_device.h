@@ -188,6 +188,12 @@ template <bool EXACT>
 __device__ __forceinline__ bool slab(const DNode& n, v3 o, v3 d, v3 y, double max_t) {
   return slab<EXACT>(n.mn, n.mx, o, d, y, max_t);
 }
+// exact chosen per segment at run time (one copy of the walk; non-fast segments are rare)
+__device__ __forceinline__ bool slab_rt(const double* mn, const double* mx, v3 o, v3 d, v3 y, double max_t,
+                                        bool exact) {
+  if (__builtin_expect(exact, 0)) return slab<true>(mn, mx, o, d, y, max_t);
+  return slab<false>(mn, mx, o, d, y, max_t);
+}
 // May the segment (o, d) use qdiv?  Quotients (n - o) / d then stay in [2^-852, 2^820] or 0.
 __device__ __forceinline__ bool segment_fast(const KParams& kp, v3 o, v3 d) {
   return kp.fast_div && in_fast_range(o.x) && in_fast_range(o.y) && in_fast_range(o.z) &&
@@ -345,11 +351,11 @@ __device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int c
 // is left; the oversized leaves are tested directly from a short list, merged in by their
 // left-first ordinal.  The reference's root test comes first, so rays outside the scene still
 // cost one box test.
-template <bool ANY, bool EXACT, bool COUNT>
+template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
-                                               double& hb1, double& hb2, Counters& cn) {
+                                               double& hb1, double& hb2, Counters& cn, bool exact) {
   if (COUNT) cn.bbox++;
-  if (!slab<EXACT>(kp.nodes[0], o, d, y, max_t)) return false;
+  if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return false;
   const v3 e = o + vmul(d, max_t);  // far end point (cull only; max_t only shrinks below)
   bool hit = false;
   int bi = 0;
@@ -365,7 +371,7 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
       const DBig& bg = kp.big[bi];
       // primitives first: an oversized leaf's box (the room) passes for almost every segment
       if (leaf_may_hit<COUNT>(kp, bg.first, bg.count, o, e, cn) && (COUNT ? (cn.bbox++, true) : true) &&
-          slab<EXACT>(bg.mn, bg.mx, o, d, y, max_t) &&
+          slab_rt(bg.mn, bg.mx, o, d, y, max_t, exact) &&
           leaf_prims_cull<ANY, COUNT>(kp, bg.first, bg.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
         hit = true;
         if (ANY) return true;
@@ -375,7 +381,7 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
     }
     if (!more) break;
     if (COUNT) cn.bbox++;
-    if (!slab<EXACT>(n, o, d, y, max_t)) { node = n.skip; continue; }
+    if (!slab_rt(n.mn, n.mx, o, d, y, max_t, exact)) { node = n.skip; continue; }
     if (n.count == 0) { node = node + 1; continue; }
     if (leaf_prims_cull<ANY, COUNT>(kp, n.first, n.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
       hit = true;
@@ -454,9 +460,10 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
     const bool fast = segment_fast(kp, o, d);
     RRT_T0(tt0);
     bool hit;
-    if (opt && kp.clean_nodes)
-      hit = fast ? traverse_clean<ANY, false, COUNT>(kp, o, d, y, seg_t, slot, b1, b2, cn)
-                 : traverse_clean<ANY, true, COUNT>(kp, o, d, y, seg_t, slot, b1, b2, cn);
+    if (!COUNT)  // the clean tree, or the reference tree itself with no oversized list (host)
+      hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
+    else if (kp.count_exec)
+      hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
     else
       hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                  : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);

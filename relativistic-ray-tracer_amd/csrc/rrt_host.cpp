@@ -523,6 +523,15 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
       if (!(x == 0.0 || (a >= 0x1p-800 && a <= 0x1p20))) c->fast_div = false;
     }
   }
+  // first-leaf ordinal of every subtree (DNode.pad), for the walk's merge with the oversized list
+  std::vector<int32_t> first_ord(c->nodes.size(), 0);
+  {
+    int32_t ord = 0;
+    for (size_t i = 0; i < c->nodes.size(); ++i)  // pre-order: a subtree's first leaf comes first
+      if (c->nodes[i].count != 0) first_ord[i] = ord++;
+    for (size_t i = c->nodes.size(); i-- > 0;)
+      if (c->nodes[i].count == 0) first_ord[i] = first_ord[c->nodes[i].left];
+  }
   // device layout
   std::vector<DNode> dn(c->nodes.size());
   for (size_t i = 0; i < c->nodes.size(); ++i) {
@@ -530,7 +539,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     DNode& d = dn[i];
     d.mn[0] = n.bb.mn.x; d.mn[1] = n.bb.mn.y; d.mn[2] = n.bb.mn.z;
     d.mx[0] = n.bb.mx.x; d.mx[1] = n.bb.mx.y; d.mx[2] = n.bb.mx.z;
-    d.skip = n.skip; d.first = n.first; d.count = n.count; d.pad = 0;
+    d.skip = n.skip; d.first = n.first; d.count = n.count; d.pad = first_ord[i];
   }
   std::vector<DPrimGeo> geo(c->leaf.size());
   std::vector<DPrimNrm> nrm(c->leaf.size());
@@ -679,9 +688,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.cam = c->cam; kp.hole = c->hole;
   kp.grid = c->hgrid;
   kp.grid.k = (p->flags & RRT_RENDER_NO_SKIP) ? nullptr : c->d_grid;
+  // the walk always runs over a "clean" tree: the real one, or the reference tree (whose DNode
+  // pad carries the first-leaf ordinals too) with an empty oversized-leaf list
   const bool use_clean = c->has_clean && !(p->flags & RRT_RENDER_NO_CLEAN);
-  kp.clean_nodes = use_clean ? c->d_clean : nullptr;
-  kp.big = c->d_big; kp.clean_root = c->clean_root; kp.n_big = c->n_big;
+  kp.clean_nodes = use_clean ? c->d_clean : c->d_nodes;
+  kp.big = c->d_big; kp.clean_root = 0; kp.n_big = use_clean ? c->n_big : 0u;
   kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
   {
     const Box& rb = c->nodes[0].bb;

@@ -19,7 +19,7 @@ def main():
         names = {}
         for r in rows:
             k = r["Kernel_Name"]
-            if not any(s in k for s in ("render", "sample", "mega")):
+            if not any(s in k for s in ("render", "sample", "mega", "batch")):
                 continue
             did = int(r.get("Dispatch_Id", 0))
             per[did][r["Counter_Name"]] = per[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
