@@ -145,6 +145,8 @@ enum {
                                      are identical) */
   RRT_RENDER_PER_PIXEL = 1u << 7, /* depth <= 1: one lane per pixel (per-sample kernel) instead
                                      of the sample-parallel kernel (A/B testing) */
+  RRT_RENDER_ORDERED = 1u << 9,   /* sample-parallel kernel: claim tiles in list order instead
+                                     of centre-first (A/B testing) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of

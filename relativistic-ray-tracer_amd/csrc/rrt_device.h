@@ -362,32 +362,35 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
   const int nb = (int)kp.n_big;
   int next_big = nb ? kp.big[0].dfs : 0x7fffffff;
   int node = kp.clean_root;
+  // one item per iteration -- the next oversized leaf if it comes before the current node's
+  // subtree in left-first order, else the node -- so both kinds share one box test and one
+  // primitive loop (one set of temporaries)
   for (;;) {
     const bool more = node >= 0;
-    DNode n;
-    if (more) n = kp.clean_nodes[node];
-    const int lim = more ? n.pad : 0x7fffffff;  // pad = left-first ordinal of the subtree's first leaf
-    while (next_big < lim) {                    // oversized leaves that come first
-      const DBig& bg = kp.big[bi];
-      // primitives first: an oversized leaf's box (the room) passes for almost every segment
-      if (leaf_may_hit<COUNT>(kp, bg.first, bg.count, o, e, cn) && (COUNT ? (cn.bbox++, true) : true) &&
-          slab_rt(bg.mn, bg.mx, o, d, y, max_t, exact) &&
-          leaf_prims_cull<ANY, COUNT>(kp, bg.first, bg.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
-        hit = true;
-        if (ANY) return true;
-      }
-      ++bi;
-      next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
+    const DNode* n = more ? &kp.clean_nodes[node] : nullptr;
+    const bool big = next_big < (more ? n->pad : 0x7fffffff);
+    if (!big && !more) break;
+    const double* mn = big ? kp.big[bi].mn : n->mn;
+    const double* mx = big ? kp.big[bi].mx : n->mx;
+    const int first = big ? kp.big[bi].first : n->first;
+    const int count = big ? kp.big[bi].count : n->count;
+    // an oversized leaf's box (the room) passes for almost every segment: cull its primitives
+    // by their planes first and skip the box test when none survives
+    bool pass = !big || leaf_may_hit<COUNT>(kp, first, count, o, e, cn);
+    if (pass) {
+      if (COUNT) cn.bbox++;
+      pass = slab_rt(mn, mx, o, d, y, max_t, exact);
     }
-    if (!more) break;
-    if (COUNT) cn.bbox++;
-    if (!slab_rt(n.mn, n.mx, o, d, y, max_t, exact)) { node = n.skip; continue; }
-    if (n.count == 0) { node = node + 1; continue; }
-    if (leaf_prims_cull<ANY, COUNT>(kp, n.first, n.count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
+    if (pass && count != 0 && leaf_prims_cull<ANY, COUNT>(kp, first, count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
       hit = true;
       if (ANY) return true;
     }
-    node = n.skip;
+    if (big) {
+      ++bi;
+      next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
+    } else {
+      node = (pass && count == 0) ? node + 1 : n->skip;
+    }
   }
   return hit;
 }
@@ -491,6 +494,19 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   }
   RRT_ACC(t_query, tq0);
   return false;
+}
+
+// query() behind a call: the caller keeps only what is live across the call, the walk gets the
+// register file to itself (rrt_sample.hip batch kernel)
+template <bool ANY>
+__device__ __noinline__ bool query_call(const KParams& kp, v3 o, v3 d, Isect* is) {
+  Counters cn = {};
+  return query<ANY, false>(kp, o, d, is, cn);
+}
+template <bool ANY, bool COUNT, bool NI>
+__device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  if (NI && !COUNT) return query_call<ANY>(kp, o, d, is);
+  return query<ANY, COUNT>(kp, o, d, is, cn);
 }
 
 // ------------------------------------------------------------------ BSDFs (bsdf.cpp / bsdf.h)

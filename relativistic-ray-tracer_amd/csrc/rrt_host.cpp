@@ -119,6 +119,8 @@ struct rrt_ctx {
   uint32_t* d_counter = nullptr;
   uint32_t* d_tiles = nullptr;
   size_t tiles_cap = 0;
+  uint32_t* d_order = nullptr;  // batch kernel: tile claim order
+  size_t order_cap = 0;
   float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
   size_t px_cap = 0;
   float last_ms = 0.f;
@@ -182,7 +184,7 @@ void rrt_destroy(rrt_ctx* c) {
   if (c->device >= 0) {
     hipSetDevice(c->device);
     free_scene_dev(c);
-    hipFree(c->d_counter); hipFree(c->d_tiles); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
+    hipFree(c->d_counter); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -754,6 +756,28 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     while (gsz < want_g) gsz <<= 1;
     kp.group = gsz;
     kp.n_pixels = n_tiles * ts * ts;
+    // Claim order: tiles nearest the frame centre first (where the geometry and the black hole's
+    // ring usually are), so the launch ends on cheap border tiles rather than on a costly
+    // region; consecutive claims stay spatially adjacent (coherent waves, warm caches).
+    std::vector<uint32_t> order(n_tiles);
+    for (uint32_t k = 0; k < n_tiles; ++k) order[k] = k;
+    if (!(p->flags & RRT_RENDER_ORDERED)) {
+      const double cx = 0.5 * p->frame_w, cy = 0.5 * p->frame_h;
+      std::vector<double> key(n_tiles);
+      for (uint32_t k = 0; k < n_tiles; ++k) {
+        const double dx = tiles[2 * k] + 0.5 * ts - cx, dy = tiles[2 * k + 1] + 0.5 * ts - cy;
+        key[k] = dx * dx + dy * dy;
+      }
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    }
+    if (c->order_cap < n_tiles) {
+      hipFree(c->d_order); c->d_order = nullptr;
+      HIPCHK(c, hipMalloc(&c->d_order, sizeof(uint32_t) * n_tiles));
+      c->order_cap = n_tiles;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_order, order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice, stream));
+    HIPCHK(c, hipStreamSynchronize(stream));  // `order` is a host temporary
+    kp.tile_order = c->d_order;
   }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);

@@ -21,6 +21,7 @@ struct ColdLds {
   double s1[256], s2[256];
   float rr[256], rg[256], rb[256];
   double hp[3][256], nn[3][256], wo[3][256];
+  uint32_t bsdf[256];
 };
 
 template <class T>
@@ -28,17 +29,21 @@ __device__ __forceinline__ void lput(T* a, uint32_t i, T v) { ((volatile T*)a)[i
 template <class T>
 __device__ __forceinline__ T lget(const T* a, uint32_t i) { return ((const volatile T*)a)[i]; }
 
-// estimate_direct_lighting_importance (part1_code.cpp:33-57); the camera-hit record is parked in
-// LDS across every shadow query and re-read per light sample.
-template <bool COUNT, bool LEAN>
-__device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
-                                      Counters& cn) {
+// park a camera-hit record in the lane's LDS slots
+__device__ __forceinline__ void park_hit(ColdLds& cl, uint32_t t, const Isect& is0) {
   for (int k = 0; k < 3; ++k) {
     lput(cl.hp[k], t, (&is0.hit_p.x)[k]);
     lput(cl.nn[k], t, (&is0.n.x)[k]);
     lput(cl.wo[k], t, (&is0.w_out.x)[k]);
   }
-  const uint32_t bsdf = (uint32_t)is0.bsdf;
+  lput(cl.bsdf, t, (uint32_t)is0.bsdf);
+}
+
+// estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
+// (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
+template <bool COUNT, bool LEAN, bool NI = false>
+__device__ spec direct_importance_parked(const KParams& kp, Rng& g, ColdLds& cl, uint32_t t, Counters& cn) {
+  const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
   int total = 0;
   for (uint32_t li = 0; li < kp.n_lights; ++li) {
@@ -55,22 +60,22 @@ __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is
       const v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
-      if (!query<true, COUNT>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
+      if (!query_nx<true, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
     }
   }
   return L / (float)total;
 }
-
-// estimate_direct_lighting_hemisphere (part1_code.cpp:15-31)
-template <bool COUNT>
-__device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
+template <bool COUNT, bool LEAN>
+__device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
-  for (int k = 0; k < 3; ++k) {
-    lput(cl.hp[k], t, (&is0.hit_p.x)[k]);
-    lput(cl.nn[k], t, (&is0.n.x)[k]);
-    lput(cl.wo[k], t, (&is0.w_out.x)[k]);
-  }
-  const uint32_t bsdf = (uint32_t)is0.bsdf;
+  park_hit(cl, t, is0);
+  return direct_importance_parked<COUNT, LEAN>(kp, g, cl, t, cn);
+}
+
+// estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
+template <bool COUNT, bool NI = false>
+__device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ColdLds& cl, uint32_t t, Counters& cn) {
+  const uint32_t bsdf = lget(cl.bsdf, t);
   const int num = (int)(kp.n_lights * kp.ns_area_light);
   spec L = S(0, 0, 0);
   for (int i = 0; i < num; ++i) {
@@ -82,10 +87,16 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
     const v3 wi_world = to_world(f, w_in);
     const spec fw = bsdf_f(kp.bsdfs[bsdf], to_local(f, wo), w_in);
     Isect is2;
-    if (query<false, COUNT>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (query_nx<false, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * fw) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
+}
+template <bool COUNT>
+__device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
+                                      Counters& cn) {
+  park_hit(cl, t, is0);
+  return direct_hemisphere_parked<COUNT>(kp, g, cl, t, cn);
 }
 
 }  // namespace rrt
@@ -268,18 +279,31 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
 // group leader folds the samples into the pixel sums in sample order (the reference's float /
 // double accumulation order) with the adaptive stop test at every samples_per_batch boundary;
 // samples past the stop are discarded with their draws.  Results equal the sequential loop's.
+#ifndef RRT_BATCH_CALL
+#define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
+#endif
+
+// Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
+// run with only the lane's own few speculation registers live.
+struct GroupLds {
+  uint64_t key[128];
+  uint32_t px[128], py[128], slot[128], O[128], i[128], hyp[128];
+  float rr[128], rg[128], rb[128];
+  double s1[128], s2[128];
+};
+
 template <bool LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
   using namespace rrt;
   __shared__ ColdLds cl;
+  __shared__ GroupLds gs;
   __shared__ float fr[256], fg[256], fb[256];
   const uint32_t t = threadIdx.x;
   const uint32_t lane = t & 63u;
   const uint32_t G = kp.group;
   const uint32_t gl = lane & (G - 1u);
   const uint32_t gbase = lane - gl;
-  const uint64_t gmask = ((G >= 64u) ? ~0ull : ((1ull << G) - 1ull)) << gbase;
-  const uint64_t ltmask = gmask & ((1ull << lane) - 1ull);
+  const uint32_t gid = t / G;  // group slot in GroupLds
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit;
   const DCamera& cam = kp.cam;
@@ -289,12 +313,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
   uint32_t prof_blocks = 0, prof_samples = 0;  // pixels claimed, query rounds
 #endif
 
-  bool have = false, done = false, hyp = false;
-  uint32_t px = 0, py = 0, slot = 0, O = 0;
-  int i = 0;
-  uint64_t key = 0;
-  spec ret = S(0, 0, 0);  // group leader only
-  double s1 = 0.0, s2 = 0.0;
+  bool have = false, done = false;
 
   for (;;) {
     // ---- claim a pixel (one atomic per group)
@@ -311,42 +330,52 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
 #if RRT_PROFILE
         ++prof_blocks;
 #endif
-        const uint32_t tl = p / tpix, r = p % tpix, lx = r % ts, ly = r / ts;
+        const uint32_t tl = kp.tile_order[p / tpix], r = p % tpix, lx = r % ts, ly = r / ts;
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
         if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
-          px = x; py = y; slot = p; key = rrt_pixel_key(kp.seed, x, y);
-          O = 0; i = 0; hyp = false; ret = S(0, 0, 0); s1 = 0.0; s2 = 0.0;
+          if (gl == 0) {
+            lput(gs.px, gid, x); lput(gs.py, gid, y); lput(gs.slot, gid, tl * tpix + r);
+            lput(gs.key, gid, rrt_pixel_key(kp.seed, x, y));
+            lput(gs.O, gid, 0u); lput(gs.i, gid, 0u); lput(gs.hyp, gid, 0u);
+            lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
+            lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
+          }
           have = true;
         }
       }
     }
     if (__ballot(!done) == 0) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ---- camera queries at speculated draw offsets, re-run until the offsets are consistent
-    const int left = (int)kp.ns_aa - i;
+    const int left = (int)kp.ns_aa - (int)lget(gs.i, gid);
     const bool act = have && (int)gl < left;
-    bool valid = false, hit = false, h = hyp;
+    bool valid = false, hit = false, h = lget(gs.hyp, gid) != 0;
     uint32_t off = 0;
-    Isect is;
     for (;;) {
       const bool need = act && !valid;
       if (__ballot(need) == 0) break;
 #if RRT_PROFILE
       ++prof_samples;
 #endif
-      const uint32_t nh = (uint32_t)__popcll(__ballot(act && h) & ltmask);
+      const uint64_t lt = ((1ull << lane) - 1ull) & ~((1ull << gbase) - 1ull);  // group lanes before me
+      const uint32_t nh = (uint32_t)__popcll(__ballot(act && h) & lt);
       if (need) {
-        off = O + nh * Dh + (gl - nh) * Dm;
-        Rng g; g.key = key; g.ctr = off;
+        off = lget(gs.O, gid) + nh * Dh + (gl - nh) * Dm;
+        Rng g; g.key = lget(gs.key, gid); g.ctr = off;
         double jx, jy; g.grid(jx, jy);
-        const double sx = (double)px + jx, sy = (double)py + jy;
+        const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
         const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;  // Camera::generate_ray (:182-187)
         const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
         const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
-        hit = query<false, false>(kp, ld3(cam.pos), unit(w), &is, cn);
+        Isect is;
+        hit = query_nx<false, false, RRT_BATCH_CALL>(kp, ld3(cam.pos), unit(w), &is, cn);
+        if (hit) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
       }
-      const uint32_t na = (uint32_t)__popcll(__ballot(act && hit) & ltmask);
-      valid = act && (O + na * Dh + (gl - na) * Dm == off);
+      const uint32_t na = (uint32_t)__popcll(__ballot(act && hit) & lt);
+      valid = act && (lget(gs.O, gid) + na * Dh + (gl - na) * Dm == off);
       h = hit;
     }
     const uint64_t hits = __ballot(act && hit);
@@ -354,12 +383,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
     // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
     spec s = S(0, 0, 0);
     if (act && hit) {
-      Rng g; g.key = key; g.ctr = off + Dm;
-      const spec e = emission(kp.bsdfs[is.bsdf]);
+      Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
+      const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (LEAN) s = e + direct_importance_lds<false, true>(kp, g, is, cl, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<false>(kp, g, is, cl, t, cn);
-      else s = e + direct_importance_lds<false, false>(kp, g, is, cl, t, cn);
+      else if (LEAN) s = e + direct_importance_parked<false, true, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, false, RRT_BATCH_CALL>(kp, g, cl, t, cn);
     }
     if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -370,6 +399,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
     uint32_t stop = 0;
     if (have && gl == 0) {
       const int n = left < (int)G ? left : (int)G;
+      spec ret = S(lget(gs.rr, gid), lget(gs.rg, gid), lget(gs.rb, gid));
+      double s1 = lget(gs.s1, gid), s2 = lget(gs.s2, gid);
+      int i = (int)lget(gs.i, gid);
+      uint32_t O = lget(gs.O, gid), hyp = 0;
       for (int k = 0; k < n; ++k) {
         const spec sk = S(lget(fr, t + k), lget(fg, t + k), lget(fb, t + k));
         ret = ret + sk;
@@ -379,7 +412,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
         ++i;
         const bool hk = (hits >> (gbase + k)) & 1ull;
         O += hk ? Dh : Dm;
-        hyp = hk;
+        hyp = hk ? 1u : 0u;
         bool st = i >= (int)kp.ns_aa;
         if ((uint32_t)i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
           const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
@@ -388,16 +421,18 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
         if (st) { stop = 1; break; }
       }
       if (stop) {
+        const uint32_t slot = lget(gs.slot, gid);
         const spec r = ret / (float)i;
         kp.rgb[3 * slot] = r.r; kp.rgb[3 * slot + 1] = r.g; kp.rgb[3 * slot + 2] = r.b;
         kp.count[slot] = i;
         if (kp.draws) kp.draws[slot] = O;
+      } else {
+        lput(gs.rr, gid, ret.r); lput(gs.rg, gid, ret.g); lput(gs.rb, gid, ret.b);
+        lput(gs.s1, gid, s1); lput(gs.s2, gid, s2);
+        lput(gs.i, gid, (uint32_t)i); lput(gs.O, gid, O); lput(gs.hyp, gid, hyp);
       }
     }
     stop = __shfl(stop, (int)gbase);
-    i = __shfl(i, (int)gbase);
-    O = __shfl(O, (int)gbase);
-    hyp = __shfl((uint32_t)hyp, (int)gbase) != 0;
     if (stop) have = false;
   }
 #if RRT_PROFILE
