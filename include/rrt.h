@@ -147,6 +147,8 @@ enum {
                                      of the sample-parallel kernel (A/B testing) */
   RRT_RENDER_ORDERED = 1u << 9,   /* sample-parallel kernel: claim tiles in list order instead
                                      of centre-first (A/B testing) */
+  RRT_RENDER_NO_FIRST = 1u << 10, /* sample-parallel kernel: no sample-0 pre-pass (speculate
+                                     "miss" for a pixel's first step; A/B testing) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of

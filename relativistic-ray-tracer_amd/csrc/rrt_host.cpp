@@ -20,11 +20,12 @@
 #include "../../include/rrt_scene_format.h"
 #include "rrt_internal.h"
 
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, int waves, uint32_t grid,
+hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream);
-hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream);
-hipError_t rrt_launch_sample(const KParams& kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
-hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_mega(const KParams& kp, const KParams* d_kp, int count, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -116,11 +117,14 @@ struct rrt_ctx {
   std::vector<DBig> big;
   uint64_t device_bytes = 0;
   // per-launch workspace
+  KParams* d_kp = nullptr;  // the launch's parameters (kernels take them by pointer)
   uint32_t* d_counter = nullptr;
   uint32_t* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_order = nullptr;  // batch kernel: tile claim order
   size_t order_cap = 0;
+  KParams::FirstSample* d_first = nullptr;  // batch kernel: sample 0 per pixel slot
+  size_t first_cap = 0;
   float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
   size_t px_cap = 0;
   float last_ms = 0.f;
@@ -169,7 +173,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counter, 64) != hipSuccess) {
+        hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
       return RRT_E_HIP;
     }
@@ -184,7 +188,7 @@ void rrt_destroy(rrt_ctx* c) {
   if (c->device >= 0) {
     hipSetDevice(c->device);
     free_scene_dev(c);
-    hipFree(c->d_counter); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
+    hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -728,14 +732,15 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
   const int lean = (!deep && !count && c->lean && !p->direct_hemisphere) ? 1 : 0;
   const uint32_t wv = p->variant & 0xffu;
-  const int waves = (wv >= 1 && wv <= 5) ? (int)wv : (pixel_loop || mega ? 2 : 3);
+  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
   // Sample-parallel kernel (rrt_sample.hip rrt_batch_kernel) whenever a pixel takes more than
   // one sample: it needs each camera sample's RNG draw count to depend only on whether its query
   // hit, which holds at depth <= 1 (jitter + the direct-lighting samplers).
-  const bool batch = !deep && !count && !mega && !pixel_loop && p->ns_aa >= 2 && !(p->flags & RRT_RENDER_PER_PIXEL);
+  const bool batch = !deep && !count && !mega && !pixel_loop && std::min(p->ns_aa, p->samples_per_batch) >= 5 &&
+                     !(p->flags & RRT_RENDER_PER_PIXEL);
   if (batch) {
     kp.draws_miss = 2;
     uint32_t dh = 2;
@@ -751,7 +756,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       }
     }
     kp.draws_hit = dh;
-    uint32_t gsz = 2;
+    uint32_t gsz = 8;  // groups of 8..32 lanes (GroupLds holds 32 groups per block)
     const uint32_t want_g = std::min<uint32_t>(std::min<uint32_t>(p->ns_aa, p->samples_per_batch), 32u);
     while (gsz < want_g) gsz <<= 1;
     kp.group = gsz;
@@ -778,27 +783,42 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     HIPCHK(c, hipMemcpyAsync(c->d_order, order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice, stream));
     HIPCHK(c, hipStreamSynchronize(stream));  // `order` is a host temporary
     kp.tile_order = c->d_order;
+    kp.first = nullptr;
+    if (!(p->flags & RRT_RENDER_NO_FIRST)) {
+      if (c->first_cap < kp.n_pixels) {
+        hipFree(c->d_first); c->d_first = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_first, sizeof(KParams::FirstSample) * kp.n_pixels));
+        c->first_cap = kp.n_pixels;
+      }
+      kp.first = c->d_first;
+    }
   }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (grid == 0) grid = 1;
   c->last_grid = grid;
+  HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   HIPCHK(c, hipEventRecord(c->ev0, stream));
   const char* tf[2] = {"false", "true"};
   char name[64];
   if (batch) {
-    const int w = lean ? (waves == 2 || waves == 4 ? waves : 3) : 2;
+    // 5 waves/SIMD measured best on cfg3 (spills are cheap; latency hiding is not)
+    const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
+    const int w = lean ? bw : 2;
     std::snprintf(name, sizeof(name), "rrt_batch_kernel<%s, %d>", tf[lean], w);
-    HIPCHK(c, rrt_launch_batch(kp, lean, waves, grid, stream));
+    if (kp.first)
+      HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
+                                 stream));
+    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, bw, grid, stream));
   } else if (mega) {
     std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
-    HIPCHK(c, rrt_launch_mega(kp, count, waves, grid, stream));
+    HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %s, ...>", tf[deep], tf[count], tf[lean]);
-    HIPCHK(c, rrt_launch_render(kp, deep, count, lean, waves, grid, stream));
+    HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {
     std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %s, ...>", tf[count], tf[lean]);
-    HIPCHK(c, rrt_launch_sample(kp, count, lean, waves, grid, stream));
+    HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }
   c->last_kernel = name;
   HIPCHK(c, hipEventRecord(c->ev1, stream));

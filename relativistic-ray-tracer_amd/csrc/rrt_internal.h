@@ -116,6 +116,8 @@ struct KParams {
   // sample-parallel kernel (rrt_sample.hip rrt_batch_kernel)
   uint32_t n_pixels;     // n_tiles * tile_size^2 (pixel work items)
   const uint32_t* tile_order;  // claim order over the caller's tile list
+  struct FirstSample { float r, g, b; uint32_t hit; };
+  FirstSample* first;          // sample 0 of every pixel slot (rrt_first_kernel), or null
   uint32_t group;        // lanes per pixel (power of two, 2..32)
   uint32_t draws_miss;   // RNG draws of a camera sample whose query misses (jitter: 2)
   uint32_t draws_hit;    // ... and of one that hits (jitter + the direct-lighting sampler draws)

@@ -163,7 +163,8 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
 // only, no microfacet BSDF, importance-sampled direct light (the BASELINE scenes); WAVES: the
 // register budget, as minimum waves per SIMD.
 template <bool DEEP, bool COUNT, bool LEAN, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(KParams kp) {
+__global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
   using namespace rrt;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t bpt = kp.blocks_per_tile_side;
@@ -229,9 +230,9 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
 // ------------------------------------------------------------------ launch shims (C++ linkage)
 // Kernel selection: deep / counting variants are built once (1 wave per SIMD budget); the
 // depth <= 1 path has general and LEAN builds at 1..4 waves per SIMD (A/B knob `waves`).
-hipError_t rrt_launch_render(const KParams& kp, int deep, int count, int lean, int waves, uint32_t grid,
+hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream) {
-#define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, kp)
+#define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
   if (deep) {
     if (count) RRT_LAUNCH(true, true, false, 1); else RRT_LAUNCH(true, false, false, 1);
   } else if (count) {

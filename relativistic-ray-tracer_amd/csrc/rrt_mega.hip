@@ -62,7 +62,8 @@ enum : uint32_t { Q_CAMERA = 0, Q_SHADOW = 1, Q_HEMI = 2 };
 }  // namespace rrt
 
 template <bool COUNT, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(KParams kp) {
+__global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
   using namespace rrt;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
@@ -293,11 +294,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(KParams kp) {
 }
 
 // waves: minimum waves per SIMD the register allocation must allow (1..4); A/B knob
-hipError_t rrt_launch_mega(const KParams& kp, int count, int waves, uint32_t grid, hipStream_t stream) {
+hipError_t rrt_launch_mega(const KParams& kp, const KParams* d_kp, int count, int waves, uint32_t grid, hipStream_t stream) {
 #define RRT_MEGA_CASE(W)                                                                         \
   case W:                                                                                        \
-    if (count) hipLaunchKernelGGL((rrt_mega_kernel<true, W>), dim3(grid), dim3(256), 0, stream, kp); \
-    else hipLaunchKernelGGL((rrt_mega_kernel<false, W>), dim3(grid), dim3(256), 0, stream, kp);      \
+    if (count) hipLaunchKernelGGL((rrt_mega_kernel<true, W>), dim3(grid), dim3(256), 0, stream, d_kp); \
+    else hipLaunchKernelGGL((rrt_mega_kernel<false, W>), dim3(grid), dim3(256), 0, stream, d_kp);      \
     break;
   switch (waves) {
     RRT_MEGA_CASE(1)

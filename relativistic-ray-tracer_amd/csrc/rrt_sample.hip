@@ -17,11 +17,15 @@
 namespace rrt {
 
 // per-lane LDS slots, structure-of-arrays (consecutive lanes hit consecutive banks)
-struct ColdLds {
-  double s1[256], s2[256];
-  float rr[256], rg[256], rb[256];
+struct ShadeLds {  // the camera hit being shaded, parked across its shadow queries
   double hp[3][256], nn[3][256], wo[3][256];
   uint32_t bsdf[256];
+  float cr[256], cg[256], cb[256];  // a light sample's contribution, parked across its shadow query
+                                    // (the batch kernel's fold then reads each sample's radiance here)
+};
+struct ColdLds : ShadeLds {  // + the per-pixel sums of the lane-per-pixel kernel
+  double s1[256], s2[256];
+  float rr[256], rg[256], rb[256];
 };
 
 template <class T>
@@ -30,7 +34,7 @@ template <class T>
 __device__ __forceinline__ T lget(const T* a, uint32_t i) { return ((const volatile T*)a)[i]; }
 
 // park a camera-hit record in the lane's LDS slots
-__device__ __forceinline__ void park_hit(ColdLds& cl, uint32_t t, const Isect& is0) {
+__device__ __forceinline__ void park_hit(ShadeLds& cl, uint32_t t, const Isect& is0) {
   for (int k = 0; k < 3; ++k) {
     lput(cl.hp[k], t, (&is0.hit_p.x)[k]);
     lput(cl.nn[k], t, (&is0.n.x)[k]);
@@ -42,7 +46,7 @@ __device__ __forceinline__ void park_hit(ColdLds& cl, uint32_t t, const Isect& i
 // estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
 template <bool COUNT, bool LEAN, bool NI = false>
-__device__ spec direct_importance_parked(const KParams& kp, Rng& g, ColdLds& cl, uint32_t t, Counters& cn) {
+__device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
   int total = 0;
@@ -60,7 +64,10 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ColdLds& cl,
       const v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
-      if (!query_nx<true, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
+      // only the loop state and the RNG stay in registers across the shadow query
+      lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
+      if (!query_nx<true, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
+        L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
     }
   }
   return L / (float)total;
@@ -74,7 +81,7 @@ __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is
 
 // estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
 template <bool COUNT, bool NI = false>
-__device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ColdLds& cl, uint32_t t, Counters& cn) {
+__device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   const int num = (int)(kp.n_lights * kp.ns_area_light);
   spec L = S(0, 0, 0);
@@ -119,7 +126,8 @@ extern "C" int rrt_prof_read(unsigned long long* out) {  // out: 8 + 3 * 16384
 // COUNT: per-pixel work counters; LEAN: area lights only, no microfacet BSDF, importance-sampled
 // direct light (the BASELINE scenes); WAVES: register budget (minimum waves per SIMD).
 template <bool COUNT, bool LEAN, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
+__global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
   using namespace rrt;
   __shared__ ColdLds cl;
   const uint32_t t = threadIdx.x;
@@ -285,19 +293,22 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(KParams kp) {
 
 // Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
 // run with only the lane's own few speculation registers live.
-struct GroupLds {
-  uint64_t key[128];
-  uint32_t px[128], py[128], slot[128], O[128], i[128], hyp[128];
-  float rr[128], rg[128], rb[128];
-  double s1[128], s2[128];
+struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
+  uint64_t key[32];
+  uint32_t px[32], py[32], slot[32], O[32], i[32], hyp[32];
+  float rr[32], rg[32], rb[32];
+  double s1[32], s2[32];
 };
 
 template <bool LEAN, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
+__global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
   using namespace rrt;
-  __shared__ ColdLds cl;
+  __shared__ ShadeLds cl;
   __shared__ GroupLds gs;
-  __shared__ float fr[256], fg[256], fb[256];
+  float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
+  float* const fg = cl.cg;
+  float* const fb = cl.cb;
   const uint32_t t = threadIdx.x;
   const uint32_t lane = t & 63u;
   const uint32_t G = kp.group;
@@ -334,11 +345,23 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
         if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
           if (gl == 0) {
-            lput(gs.px, gid, x); lput(gs.py, gid, y); lput(gs.slot, gid, tl * tpix + r);
+            const uint32_t slot = tl * tpix + r;
+            lput(gs.px, gid, x); lput(gs.py, gid, y); lput(gs.slot, gid, slot);
             lput(gs.key, gid, rrt_pixel_key(kp.seed, x, y));
-            lput(gs.O, gid, 0u); lput(gs.i, gid, 0u); lput(gs.hyp, gid, 0u);
-            lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
-            lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
+            if (kp.first) {  // sample 0 from rrt_first_kernel; its hit status is the hypothesis
+              const KParams::FirstSample f0 = kp.first[slot];
+              const spec s0 = S(f0.r, f0.g, f0.b);
+              const spec ret = S(0, 0, 0) + s0;
+              const double il = illum(s0);
+              lput(gs.rr, gid, ret.r); lput(gs.rg, gid, ret.g); lput(gs.rb, gid, ret.b);
+              lput(gs.s1, gid, 0.0 + il); lput(gs.s2, gid, 0.0 + il * il);
+              lput(gs.i, gid, 1u); lput(gs.O, gid, f0.hit ? Dh : Dm); lput(gs.hyp, gid, f0.hit);
+            } else {
+              lput(gs.O, gid, 0u); lput(gs.i, gid, 0u);
+              lput(gs.hyp, gid, 0u);  // speculate "miss"
+              lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
+              lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
+            }
           }
           have = true;
         }
@@ -350,7 +373,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ---- camera queries at speculated draw offsets, re-run until the offsets are consistent
-    const int left = (int)kp.ns_aa - (int)lget(gs.i, gid);
+    // samples this step: up to the next adaptive check (no sample past a possible stop), at most G
+    const int done_i = (int)lget(gs.i, gid);
+    const int to_check = (int)kp.samples_per_batch - done_i % (int)kp.samples_per_batch;
+    const int left = min((int)kp.ns_aa - done_i, to_check);
     const bool act = have && (int)gl < left;
     bool valid = false, hit = false, h = lget(gs.hyp, gid) != 0;
     uint32_t off = 0;
@@ -458,13 +484,62 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(KParams kp) {
 #endif
 }
 
-hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
-#define RRT_LAUNCH_B(L, W) hipLaunchKernelGGL((rrt_batch_kernel<L, W>), dim3(grid), dim3(256), 0, stream, kp)
+// Sample 0 of every pixel, one lane per pixel (tile-list order, so a wave covers two rows of a
+// tile).  Its draw offset is always 0, so it needs no speculation; its hit status then seeds the
+// batch kernel's hypothesis for the pixel's other samples (all-hit and all-miss pixels -- 99.9%
+// of cfg3 -- then need a single round), and its radiance is the first term of the pixel's sums.
+template <bool LEAN>
+__global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
+  using namespace rrt;
+  __shared__ ShadeLds cl;
+  const uint32_t t = threadIdx.x;
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  const DCamera& cam = kp.cam;
+  Counters cn = {};
+  for (uint32_t p = blockIdx.x * blockDim.x + t; p < kp.n_pixels; p += gridDim.x * blockDim.x) {
+    const uint32_t tl = p / tpix, r = p % tpix, lx = r % ts, ly = r / ts;
+    const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
+    if (!(x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1)) continue;
+    Rng g; g.key = rrt_pixel_key(kp.seed, x, y); g.ctr = 0;
+    double jx, jy; g.grid(jx, jy);
+    const double sx = (double)x + jx, sy = (double)y + jy;
+    const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;  // Camera::generate_ray (:182-187)
+    const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+    const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+    Isect is;
+    const bool hit = query<false, false>(kp, ld3(cam.pos), unit(w), &is, cn);
+    spec s = S(0, 0, 0);
+    if (hit) {
+      park_hit(cl, t, is);
+      g.ctr = kp.draws_miss;
+      const spec e = emission(kp.bsdfs[is.bsdf]);
+      if (kp.max_ray_depth == 0) s = e;
+      else if (LEAN) s = e + direct_importance_parked<false, true>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, false>(kp, g, cl, t, cn);
+    }
+    KParams::FirstSample f0;
+    f0.r = s.r; f0.g = s.g; f0.b = s.b; f0.hit = hit ? 1u : 0u;
+    kp.first[p] = f0;
+  }
+}
+
+hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, uint32_t grid, hipStream_t stream) {
+  if (lean) hipLaunchKernelGGL((rrt_first_kernel<true>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else hipLaunchKernelGGL((rrt_first_kernel<false>), dim3(grid), dim3(256), 0, stream, d_kp);
+  return hipGetLastError();
+}
+
+hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
+#define RRT_LAUNCH_B(L, W) hipLaunchKernelGGL((rrt_batch_kernel<L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
   if (lean) {
     switch (waves) {
       case 2: RRT_LAUNCH_B(true, 2); break;
-      case 4: RRT_LAUNCH_B(true, 4); break;
-      default: RRT_LAUNCH_B(true, 3); break;
+      case 3: RRT_LAUNCH_B(true, 3); break;
+      case 5: RRT_LAUNCH_B(true, 5); break;
+      case 6: RRT_LAUNCH_B(true, 6); break;
+      default: RRT_LAUNCH_B(true, 5); break;
     }
   } else {
     RRT_LAUNCH_B(false, 2);
@@ -473,8 +548,8 @@ hipError_t rrt_launch_batch(const KParams& kp, int lean, int waves, uint32_t gri
   return hipGetLastError();
 }
 
-hipError_t rrt_launch_sample(const KParams& kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream) {
-#define RRT_LAUNCH(C, L, W) hipLaunchKernelGGL((rrt_sample_kernel<C, L, W>), dim3(grid), dim3(256), 0, stream, kp)
+hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream) {
+#define RRT_LAUNCH(C, L, W) hipLaunchKernelGGL((rrt_sample_kernel<C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
   if (count) {
     RRT_LAUNCH(true, false, 1);
   } else if (lean) {

@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("RRT_LIB") or os.path.join(HERE, "librrt.so")  # RRT_L
 RRT_OK, RRT_E_INVALID, RRT_E_HIP, RRT_E_CANCELLED, RRT_E_NO_DEVICE, RRT_E_IO = 0, -1, -2, -3, -4, -5
 RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DIV = 1, 2, 4, 8
 RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_PIXEL = 16, 32, 64, 128
-RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED = 256, 512
+RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED, RRT_RENDER_NO_FIRST = 256, 512, 1024
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 
