@@ -204,7 +204,7 @@ typedef struct {
   float grid_free_frac;       /* fraction of grid cells with free radius > 0 */
   float last_kernel_ms;       /* HIP-event time of the last render launch */
   uint32_t grid_blocks, block_threads;
-  char kernel[48];            /* name of the last render kernel launched */
+  char kernel[64];            /* name of the last render kernel(s) launched */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 /* Host copy of the flattened BVH: boxes [n][6] (min, max), nodes [n][4] (first, count, left,

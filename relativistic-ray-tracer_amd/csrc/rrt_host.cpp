@@ -805,7 +805,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // 5 waves/SIMD measured best on cfg3 (spills are cheap; latency hiding is not)
     const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
     const int w = lean ? bw : 2;
-    std::snprintf(name, sizeof(name), "rrt_batch_kernel<%s, %d>", tf[lean], w);
+    std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%s, %d>", kp.first ? (lean ? "rrt_first_kernel<true> + " : "rrt_first_kernel<false> + ") : "", tf[lean], w);
     if (kp.first)
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));

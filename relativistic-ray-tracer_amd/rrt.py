@@ -60,7 +60,7 @@ class Stats(C.Structure):
                 ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("grid_n", C.c_uint32 * 3),
                 ("n_clean", C.c_uint32), ("n_big", C.c_uint32),
                 ("grid_free_frac", C.c_float), ("last_kernel_ms", C.c_float), ("grid_blocks", C.c_uint32),
-                ("block_threads", C.c_uint32), ("kernel", C.c_char * 48)]
+                ("block_threads", C.c_uint32), ("kernel", C.c_char * 64)]
 
 
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)

@@ -16,7 +16,7 @@ def kernel_values(d, counter):
         k = r["Kernel_Name"]
         if r["Counter_Name"] != counter or not k.startswith("void rrt_"):
             continue
-        if not any(s in k for s in ("batch", "sample", "render_kernel", "mega")):
+        if not any(s in k for s in ("batch", "first", "sample", "render_kernel", "mega")):
             continue
         name = k[len("void "):].split("(")[0]
         did = int(r["Dispatch_Id"])
@@ -33,11 +33,14 @@ def main():
     ap.add_argument("--out", default="gpurun_out/traffic.json")
     a = ap.parse_args()
     fetch, write = kernel_values(a.fetch, "FETCH_SIZE"), kernel_values(a.write, "WRITE_SIZE")
-    name = max(fetch, key=lambda n: fetch[n]) if fetch else None
-    if name is None:
+    if not fetch:
         raise SystemExit("no render-kernel dispatch in the PMC output")
-    fkb, wkb = fetch[name], write.get(name, 0.0)
-    out = {"workload": a.workload, "kernel": name, "fetch_size_kb": fkb, "write_size_kb": wkb,
+    # one render launch = the sample-0 pre-pass (if any) + the main kernel
+    names = sorted(fetch, key=lambda n: (0 if n.startswith("rrt_first") else 1, n))
+    fkb = sum(fetch[n] for n in names)
+    wkb = sum(write.get(n, 0.0) for n in names)
+    out = {"workload": a.workload, "kernel": " + ".join(names), "fetch_size_kb": fkb, "write_size_kb": wkb,
+           "per_kernel": {n: {"fetch_size_kb": fetch[n], "write_size_kb": write.get(n, 0.0)} for n in names},
            "hbm_bytes_per_launch": 2.0 * fkb * 1024 + wkb * 1024,
            "note": "FETCH_SIZE x 2 (gfx950 wide-read correction) + WRITE_SIZE, KB -> bytes, mean over dispatches"}
     with open(a.out, "w") as f:
