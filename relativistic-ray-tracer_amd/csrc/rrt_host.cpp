@@ -123,6 +123,7 @@ struct rrt_ctx {
   size_t tiles_cap = 0;
   uint32_t* d_order = nullptr;  // batch kernel: tile claim order
   size_t order_cap = 0;
+  std::vector<uint32_t> h_order;  // what d_order holds
   KParams::FirstSample* d_first = nullptr;  // batch kernel: sample 0 per pixel slot
   size_t first_cap = 0;
   float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
@@ -779,9 +780,13 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       hipFree(c->d_order); c->d_order = nullptr;
       HIPCHK(c, hipMalloc(&c->d_order, sizeof(uint32_t) * n_tiles));
       c->order_cap = n_tiles;
+      c->h_order.clear();
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_order, order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice, stream));
-    HIPCHK(c, hipStreamSynchronize(stream));  // `order` is a host temporary
+    if (order != c->h_order) {  // re-upload only when the tile list or its order changed
+      c->h_order = order;
+      HIPCHK(c, hipMemcpyAsync(c->d_order, c->h_order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice,
+                               stream));
+    }
     kp.tile_order = c->d_order;
     kp.first = nullptr;
     if (!(p->flags & RRT_RENDER_NO_FIRST)) {
