@@ -229,6 +229,45 @@ int rrt_scene_file_load(const char* path, rrt_scene_file** out);
 const rrt_scene_desc* rrt_scene_file_desc(const rrt_scene_file* f);
 void rrt_scene_file_free(rrt_scene_file* f);
 int rrt_camera_file_load(const char* path, rrt_camera_desc* out);
+/* .rrts writer (the layout rrt_scene_file_load reads). */
+int rrt_scene_file_save(const char* path, const rrt_scene_desc* scene);
+
+/* ---------------------------------------------------------------- native scene ingest (host only)
+ * The full CGL::Camera record: the fields Camera::dump_settings / load_settings exchange
+ * (camera.cpp:138-169), in that order; also the .rrtc payload (include/rrt_scene_format.h). */
+typedef struct {
+  double hFov, vFov, ar, nClip, fClip;
+  double pos[3], targetPos[3];
+  double phi, theta, r, minR, maxR;
+  double c2w[9];              /* row-major c2w(i, j) */
+  double screenW, screenH, screenDist;
+  double focalDistance, lensRadius;
+} rrt_camera_state;
+
+typedef struct {
+  uint32_t screen_w, screen_h;   /* -r W H (Application::resize -> Camera::set_screen_size) */
+  double lens_radius;            /* -b (AppConfig default 0.25; PathTracer::set_camera copies it) */
+  double focal_distance;         /* -d (default 4.7) */
+  uint32_t reserved[4];
+} rrt_collada_options;
+void rrt_collada_options_default(rrt_collada_options* opt);   /* 800x600, 0.25, 4.7 */
+
+/* Replaces: Collada::ColladaParser::load (collada/collada.cpp:131-936) + Application::load
+ * (application.cpp:219-295: scene objects/lights, bbox camera placement) +
+ * DynamicScene::Scene::get_static_scene (dynamic_scene/scene.cpp:133-145; halfedge vertex
+ * normals, halfEdgeMesh.cpp:29-397).  Produces the StaticScene PathTracer::set_scene receives and
+ * the Camera PathTracer::set_camera receives (cam_out may be NULL).  Host only; no GPU needed.
+ * On failure returns RRT_E_INVALID / RRT_E_IO and writes a message into err (may be NULL). */
+int rrt_collada_load(const char* path, const rrt_collada_options* opt, rrt_scene_file** scene_out,
+                     rrt_camera_state* cam_out, char* err, size_t err_len);
+/* Camera::load_settings / dump_settings text files (the `-c` flag, main.cpp). */
+int rrt_camera_settings_load(const char* path, rrt_camera_state* out);
+int rrt_camera_settings_save(const char* path, const rrt_camera_state* cam);
+/* .rrtc binary record <-> rrt_camera_state */
+int rrt_camera_state_file_load(const char* path, rrt_camera_state* out);
+int rrt_camera_state_file_save(const char* path, const rrt_camera_state* cam);
+/* The subset rrt_set_camera takes. */
+int rrt_camera_state_desc(const rrt_camera_state* cam, rrt_camera_desc* out);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@
 #include "../../include/rrt.h"
 #include "../../include/rrt_scene_format.h"
 #include "rrt_internal.h"
+#include "rrt_scene_file.h"
 
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream);
@@ -996,15 +997,6 @@ extern "C" int rrt_get_bvh(const rrt_ctx* c, double* boxes, int32_t* nodes, uint
 }
 
 // ---------------------------------------------------------------------------- file helpers
-struct rrt_scene_file {
-  std::vector<rrt_object_desc> objects;
-  std::vector<rrt_bsdf_desc> bsdfs;
-  std::vector<rrt_light_desc> lights;
-  std::vector<std::vector<double>> dbl;
-  std::vector<std::vector<uint32_t>> idx;
-  rrt_scene_desc desc{};
-};
-
 static bool rd(FILE* f, void* p, size_t n) { return std::fread(p, 1, n, f) == n; }
 
 extern "C" int rrt_scene_file_load(const char* path, rrt_scene_file** out) {
@@ -1061,12 +1053,7 @@ extern "C" int rrt_scene_file_load(const char* path, rrt_scene_file** out) {
   }
   std::fclose(f);
   if (!ok) return RRT_E_IO;
-  s->desc.n_objects = (uint32_t)s->objects.size();
-  s->desc.n_bsdfs = (uint32_t)s->bsdfs.size();
-  s->desc.n_lights = (uint32_t)s->lights.size();
-  s->desc.objects = s->objects.data();
-  s->desc.bsdfs = s->bsdfs.data();
-  s->desc.lights = s->lights.data();
+  s->finalize();
   *out = s.release();
   return RRT_OK;
 }

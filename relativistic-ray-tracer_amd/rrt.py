@@ -43,6 +43,23 @@ class CameraDesc(C.Structure):
                 ("focalDistance", C.c_double)]
 
 
+class CameraState(C.Structure):
+    """The full CGL::Camera record (Camera::dump_settings order; the .rrtc payload)."""
+    _fields_ = [("hFov", C.c_double), ("vFov", C.c_double), ("ar", C.c_double), ("nClip", C.c_double),
+                ("fClip", C.c_double), ("pos", C.c_double * 3), ("targetPos", C.c_double * 3), ("phi", C.c_double),
+                ("theta", C.c_double), ("r", C.c_double), ("minR", C.c_double), ("maxR", C.c_double),
+                ("c2w", C.c_double * 9), ("screenW", C.c_double), ("screenH", C.c_double),
+                ("screenDist", C.c_double), ("focalDistance", C.c_double), ("lensRadius", C.c_double)]
+
+    def to_array(self):
+        return np.frombuffer(bytes(self), np.float64).copy()
+
+
+class ColladaOptions(C.Structure):
+    _fields_ = [("screen_w", C.c_uint32), ("screen_h", C.c_uint32), ("lens_radius", C.c_double),
+                ("focal_distance", C.c_double), ("reserved", C.c_uint32 * 4)]
+
+
 class SpacetimeDesc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("center", C.c_double * 3), ("r_s", C.c_double),
                 ("delta_theta", C.c_double)]
@@ -67,7 +84,10 @@ class Stats(C.Structure):
 EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
            "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
            "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree",
-           "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load"]
+           "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load",
+           "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
+           "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
+           "rrt_camera_state_desc"]
 
 _lib = None
 
@@ -105,6 +125,16 @@ def lib():
         L.rrt_scene_file_desc.argtypes = [vp]
         L.rrt_scene_file_free.argtypes = [vp]
         L.rrt_camera_file_load.argtypes = [C.c_char_p, C.POINTER(CameraDesc)]
+        if hasattr(L, "rrt_collada_load"):  # absent from older builds loaded through RRT_LIB
+            L.rrt_scene_file_save.argtypes = [C.c_char_p, vp]
+            L.rrt_collada_options_default.argtypes = [C.POINTER(ColladaOptions)]
+            L.rrt_collada_load.argtypes = [C.c_char_p, C.POINTER(ColladaOptions), C.POINTER(vp),
+                                           C.POINTER(CameraState), C.c_char_p, C.c_size_t]
+            for name in ("rrt_camera_settings_load", "rrt_camera_state_file_load"):
+                getattr(L, name).argtypes = [C.c_char_p, C.POINTER(CameraState)]
+            for name in ("rrt_camera_settings_save", "rrt_camera_state_file_save"):
+                getattr(L, name).argtypes = [C.c_char_p, C.POINTER(CameraState)]
+            L.rrt_camera_state_desc.argtypes = [C.POINTER(CameraState), C.POINTER(CameraDesc)]
         _lib = L
     return _lib
 
@@ -116,15 +146,64 @@ def _p(a):
 class SceneFile:
     """A flattened static scene (.rrts, include/rrt_scene_format.h) loaded by librrt."""
 
-    def __init__(self, path):
-        h = C.c_void_p()
-        rc = lib().rrt_scene_file_load(path.encode(), C.byref(h))
-        if rc != RRT_OK:
-            raise RRTError(rc, f"cannot load scene {path}")
-        self.h = h
+    def __init__(self, path=None, handle=None):
+        if handle is None:
+            h = C.c_void_p()
+            rc = lib().rrt_scene_file_load(path.encode(), C.byref(h))
+            if rc != RRT_OK:
+                raise RRTError(rc, f"cannot load scene {path}")
+            handle = h
+        self.h = handle
 
     def desc(self):
         return lib().rrt_scene_file_desc(self.h)
+
+    def save(self, path):
+        rc = lib().rrt_scene_file_save(path.encode(), self.desc())
+        if rc != RRT_OK:
+            raise RRTError(rc, f"cannot write {path}")
+
+
+def load_collada(path, screen_w=800, screen_h=600, lens_radius=0.25, focal_distance=4.7):
+    """Native COLLADA ingest: (SceneFile, CameraState) as the reference's loader + Application::load
+    produce them for a `-r screen_w screen_h` render (include/rrt.h rrt_collada_load)."""
+    o = ColladaOptions()
+    lib().rrt_collada_options_default(C.byref(o))
+    o.screen_w, o.screen_h, o.lens_radius, o.focal_distance = screen_w, screen_h, lens_radius, focal_distance
+    h = C.c_void_p()
+    cam = CameraState()
+    err = C.create_string_buffer(512)
+    rc = lib().rrt_collada_load(path.encode(), C.byref(o), C.byref(h), C.byref(cam), err, len(err))
+    if rc != RRT_OK:
+        raise RRTError(rc, err.value.decode(errors="replace"))
+    return SceneFile(handle=h), cam
+
+
+def camera_desc(state):
+    """The rrt_set_camera subset of a CameraState."""
+    cam = CameraDesc()
+    rc = lib().rrt_camera_state_desc(C.byref(state), C.byref(cam))
+    if rc != RRT_OK:
+        raise RRTError(rc, "bad camera state")
+    return cam
+
+
+def load_camera_settings(path):
+    """Camera::load_settings text file (the `-c` flag)."""
+    st = CameraState()
+    rc = lib().rrt_camera_settings_load(path.encode(), C.byref(st))
+    if rc != RRT_OK:
+        raise RRTError(rc, f"cannot read camera settings {path}")
+    return st
+
+
+def load_camera_state(path):
+    """.rrtc record as a CameraState."""
+    st = CameraState()
+    rc = lib().rrt_camera_state_file_load(path.encode(), C.byref(st))
+    if rc != RRT_OK:
+        raise RRTError(rc, f"cannot load camera {path}")
+    return st
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
