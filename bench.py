@@ -3,9 +3,12 @@
 
 Workload (BASELINE.json configs[2], the config the metric is quoted on): CBbunny.dae at
 1920x1080, 64 spp (adaptive: batch 32, tol 0.05), Schwarzschild black hole (centre (0,1,0),
-r_s 0.1, dtheta 0.1), max_ray_depth 1 -- the reference defaults.  The scene and camera are the
-reference's own, flattened by the oracle harness (tests/golden/scenes/CBbunny.rrts,
-tests/golden/cfg3_bunny_1080p_s64/camera.rrtc); they are HBM-resident before timing.
+r_s 0.1, dtheta 0.1), max_ray_depth 1 -- the reference defaults.  The scene is the reference's
+own asset (a copy under tests/golden/dae/), read by the native COLLADA ingest
+(rrt_collada_load: byte-identical to the reference loader's scene and placed camera); scene and
+camera are HBM-resident before timing.  --workload cfg4 runs BASELINE configs[3] on the
+generated 100k-triangle torus-knot scene (rrt_scenes.py; CBdragon.dae is missing upstream) at
+3840x2160, 256 spp.
 
 One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's 32x32
 tiles are split block-cyclically (rrt_partition_tiles); every rank renders its tiles into a
@@ -33,29 +36,46 @@ import rrt_frame  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
-    "cfg3": dict(scene="scenes/CBbunny.rrts", camera="cfg3_bunny_1080p_s64/camera.rrtc", w=1920, h=1080, spp=64,
-                 bh=((0.0, 1.0, 0.0), 0.1, 0.1),
+    "cfg3": dict(dae="CBbunny.dae", w=1920, h=1080, spp=64, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=8,
                  desc="cfg3: CBbunny.dae 1920x1080 64spp, Schwarzschild geodesic (r_s 0.1, dtheta 0.1), depth 1"),
-    "cfg2": dict(scene="scenes/CBspheres_lambertian.rrts", camera="cfg2_spheres_1080p_s64_flat/camera.rrtc", w=1920,
-                 h=1080, spp=64, bh=((0.0, 1.0, 0.0), 0.0, 0.1),
-                 desc="cfg2: CBspheres_lambertian.dae 1920x1080 64spp, flat limit (r_s 0), depth 1"),
-    "cfg1": dict(scene="scenes/CBspheres_lambertian.rrts", camera="cfg1_spheres_480x360_s8/camera.rrtc", w=480,
-                 h=360, spp=8, bh=((0.0, 1.0, 0.0), 0.1, 0.1),
+    "cfg2": dict(dae="CBspheres_lambertian.dae", w=1920, h=1080, spp=64, bh=((0.0, 1.0, 0.0), 0.0, 0.1),
+                 row_stride=8, desc="cfg2: CBspheres_lambertian.dae 1920x1080 64spp, flat limit (r_s 0), depth 1"),
+    "cfg1": dict(dae="CBspheres_lambertian.dae", w=480, h=360, spp=8, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=2,
                  desc="cfg1: CBspheres_lambertian.dae 480x360 8spp, Schwarzschild"),
+    "cfg4": dict(dae="@cfg4", w=3840, h=2160, spp=256, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=32,
+                 desc="cfg4: torus knot (100k tris, CBdragon substitute) in CBempty, 3840x2160 256spp, "
+                      "Schwarzschild, depth 1"),
 }
+
+
+def load_workload_scene(wl, workdir):
+    """Native COLLADA ingest of the workload's scene -> (SceneFile, CameraState, .rrts, .rrtc)
+    (the .rrts/.rrtc copies feed the CPU baseline's restatement)."""
+    if wl["dae"].startswith("@"):
+        import rrt_scenes
+        path = os.path.join(workdir, wl["dae"][1:] + ".dae")
+        rrt_scenes.write_cfg4_dae(path)
+    else:
+        path = os.path.join(GOLD, "dae", wl["dae"])
+    scene, cam = rrt.load_collada(path, wl["w"], wl["h"])
+    spath, cpath = os.path.join(workdir, "scene.rrts"), os.path.join(workdir, "camera.rrtc")
+    scene.save(spath)
+    rc = rrt.lib().rrt_camera_state_file_save(cpath.encode(), cam)
+    assert rc == 0
+    return scene, cam, spath, cpath
 TILE = 32
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic bytes
 BYTES_PLANE = 32  # plane-cull record (DPlane) read per plane test
 
 
-def cpu_baseline(wl, threads, row_stride):
+def cpu_baseline(wl, threads, row_stride, scene_path, camera_path):
     """The oracle restatement (oracle/restate, bit-exact with the reference) on the host cores,
     over every `row_stride`-th row of the same frame (a representative bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    s = O.Scene(os.path.join(GOLD, wl["scene"]))
-    cam = O.load_camera(os.path.join(GOLD, wl["camera"]))
+    s = O.Scene(scene_path)
+    cam = O.load_camera(camera_path)
     c, r_s, dt = wl["bh"]
     p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], bh=(c[0], c[1], c[2], r_s, dt))
     rows = list(range(row_stride // 2, wl["h"], row_stride))
@@ -79,7 +99,7 @@ def main():
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-row-stride", type=int, default=8)
+    ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
                     help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic")
     a = ap.parse_args()
@@ -99,10 +119,12 @@ def main():
     wl = WORKLOADS[a.workload]
     W, H = wl["w"], wl["h"]
 
+    import tempfile
+    workdir = tempfile.mkdtemp(prefix="rrt_bench_")
     r = rrt.Renderer(device=torch.cuda.current_device())
-    scene = rrt.SceneFile(os.path.join(GOLD, wl["scene"]))
+    scene, cam_state, scene_path, camera_path = load_workload_scene(wl, workdir)
     r.set_scene(scene)
-    r.set_camera(rrt.load_camera(os.path.join(GOLD, wl["camera"])))
+    r.set_camera(rrt.camera_desc(cam_state))
     r.set_black_hole(*wl["bh"])
     params = rrt.render_params(W, H, ns_aa=wl["spp"])
 
@@ -210,7 +232,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "reference scene asset (flattened by the oracle harness), keyed RNG seed 0",
+            "data": ("generated torus-knot scene (rrt_scenes.py)" if wl["dae"].startswith("@") else
+                     "reference scene asset") + " via the native COLLADA ingest, keyed RNG seed 0",
             "config": {"workload": wl["desc"], "frame": [W, H], "spp": wl["spp"], "tile": TILE,
                        "partition": f"block-cyclic {TILE}x{TILE} tiles over {world} GPU(s), RCCL gather to rank 0"},
             "samples_per_frame": int(samples),
@@ -227,7 +250,8 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-            out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride)
+            out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride or wl["row_stride"], scene_path,
+                                               camera_path)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -20,6 +20,7 @@ thread schedule; step 4 re-renders one case with -t 1 and asserts bit-identity w
 Usage:  python3 tests/golden/make_golden.py [--only NAME ...] [--jobs 8]
 """
 import argparse
+import hashlib
 import json
 import os
 import shutil
@@ -62,7 +63,19 @@ CASES = {
     "bunnycu_96x72_s8_m2": ("CBbunny_microfacet_cu.dae", ["-s", "8", "-m", "2", "-r", "96", "72"], True),
     # a crop in cell mode (-p x y dx dy; y in sampleBuffer coordinates, y = 0 at the bottom)
     "bunny_1080p_s64_crop": ("CBbunny.dae", ["-s", "64", "-r", "1920", "1080", "-p", "896", "476", "96", "96"], True),
+    # cfg4 (BASELINE configs[3]): generated torus-knot scene (relativistic-ray-tracer_amd/rrt_scenes.py,
+    # 100k triangles in CBempty's box; CBdragon.dae is missing from the reference).  4K framing, 256 spp.
+    # (64x64 cells: the reference's -p cell mode corrupts its heap for some larger cells at 4K,
+    # e.g. 128x128 or 192x128 -- a reference bug, avoided here)
+    "cfg4_knot_4k_s256_crop": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1856", "990", "64", "64"], False),
+    "cfg4_knot_4k_s256_crop2": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1920", "990", "64", "64"], False),
+    "cfg4_knot_4k_s256_crop3": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1880", "1180", "64", "64"], False),
+    "cfg4_knot_240x135_s16": ("@cfg4", ["-s", "16", "-r", "240", "135"], True),
 }
+# generated scenes: "@name" -> writer(path) -> sha256 (the tests regenerate and check the digest)
+sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
+import rrt_scenes  # noqa: E402
+GENERATED = {"@cfg4": rrt_scenes.write_cfg4_dae}
 
 
 def run(cmd, **kw):
@@ -70,10 +83,18 @@ def run(cmd, **kw):
     subprocess.run(cmd, check=True, **kw)
 
 
+def dae_path(dae, workdir):
+    if dae in GENERATED:
+        path = os.path.join(workdir, dae[1:] + ".dae")
+        GENERATED[dae](path)
+        return path
+    return os.path.join(DAE, dae)
+
+
 def render(dae, args, workdir, threads, seed=0):
     prefix = os.path.join(workdir, "ref")
     cmd = [os.path.join(BIN, "ref_render"), "-t", str(threads), "-S", str(seed), "-O", prefix,
-           "-f", os.path.join(workdir, "out.png")] + args + [os.path.join(DAE, dae)]
+           "-f", os.path.join(workdir, "out.png")] + args + [dae_path(dae, workdir)]
     run(cmd, stdout=subprocess.DEVNULL)
     return prefix
 
@@ -112,13 +133,15 @@ def main():
         os.makedirs(out, exist_ok=True)
         with tempfile.TemporaryDirectory() as td:
             prefix = render(dae, args, td, a.jobs)
-            # scenes (and their reference BVH) are shared between cases of the same .dae
-            sdir = os.path.join(GOLD, "scenes")
+            # scenes (and their reference BVH) are shared between cases of the same .dae;
+            # generated scenes are not stored (the tests regenerate them and check the digest)
+            sdir = os.path.join(GOLD, "scenes") if dae not in GENERATED else os.path.join(td, "scenes")
             os.makedirs(sdir, exist_ok=True)
             stem = dae.replace(".dae", "")
             spath = os.path.join(sdir, stem + ".rrts")
             with open(prefix + ".rrts", "rb") as f:
                 sbytes = f.read()
+            scene_sha = hashlib.sha256(sbytes).hexdigest()
             if os.path.exists(spath):
                 with open(spath, "rb") as f:
                     assert f.read() == sbytes, f"scene dump of {dae} changed between cases"
@@ -134,13 +157,18 @@ def main():
             np.savez_compressed(os.path.join(out, "px.npz"), **px)
         meta = px["meta"]
         info = {
-            "dae": dae, "scene": "scenes/" + dae.replace(".dae", "") + ".rrts", "args": args,
+            "dae": dae, "scene": dae if dae in GENERATED else "scenes/" + dae.replace(".dae", "") + ".rrts",
+            "args": args,
             "seed": 0, "threads": a.jobs,
             "region": {"x0": int(meta[0]), "y0": int(meta[1]), "w": int(meta[2]), "h": int(meta[3])},
             "frame": {"w": int(meta[4]), "h": int(meta[5])},
             "samples": int(px["count"].astype(np.int64).sum()),
             "nonblack_fraction": float((px["rgb"].sum(-1) > 0).mean()),
         }
+        if dae in GENERATED:
+            with tempfile.TemporaryDirectory() as td:
+                info["dae_sha256"] = GENERATED[dae](os.path.join(td, "x.dae"))
+            info["rrts_sha256"] = scene_sha  # the reference loader's flattened scene
         if counters:
             info["bbox_tests"] = int(px["bbox_tests"].astype(np.int64).sum())
             info["micro_steps"] = int(px["micro_steps"].astype(np.int64).sum())

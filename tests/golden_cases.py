@@ -1,10 +1,38 @@
 """Golden cases produced by tests/golden/make_golden.py from the reference renderer."""
+import hashlib
 import json
 import os
+import sys
+import tempfile
 
 import numpy as np
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+PKG = os.path.join(os.path.dirname(GOLD), "..", "relativistic-ray-tracer_amd")
+
+
+def generated_scene(tag, want_dae_sha, want_rrts_sha):
+    """Path of the flattened scene (.rrts) of a generated asset ("@cfg4"): the generator in
+    relativistic-ray-tracer_amd/rrt_scenes.py writes the .dae (its digest must equal the one the
+    golden was rendered from), the native ingest flattens it, and the result must be byte-identical
+    to what the reference's own loader produced (digest recorded by make_golden.py)."""
+    sys.path.insert(0, PKG)
+    import rrt
+    import rrt_scenes
+    d = os.path.join(tempfile.gettempdir(), "rrt_golden_gen")
+    os.makedirs(d, exist_ok=True)
+    out = os.path.join(d, f"{tag[1:]}_{want_rrts_sha[:16]}.rrts")
+    if not os.path.exists(out):
+        dae = os.path.join(d, tag[1:] + ".dae")
+        got = {"@cfg4": rrt_scenes.write_cfg4_dae}[tag](dae)
+        assert got == want_dae_sha, f"{tag}: generated .dae differs from the golden's ({got})"
+        sc, _ = rrt.load_collada(dae)
+        tmp = out + ".tmp%d" % os.getpid()
+        sc.save(tmp)
+        os.replace(tmp, out)
+    with open(out, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == want_rrts_sha, f"{tag}: ingest differs from the reference loader"
+    return out
 
 
 def parse_args(args):
@@ -33,7 +61,10 @@ class Case:
         with open(os.path.join(self.dir, "case.json")) as f:
             self.info = json.load(f)
         self.cfg = parse_args(self.info["args"])
-        self.scene_path = os.path.join(GOLD, self.info["scene"])
+        if self.info["scene"].startswith("@"):
+            self.scene_path = generated_scene(self.info["scene"], self.info["dae_sha256"], self.info["rrts_sha256"])
+        else:
+            self.scene_path = os.path.join(GOLD, self.info["scene"])
         self.camera_path = os.path.join(self.dir, "camera.rrtc")
         self.frame_w, self.frame_h = self.info["frame"]["w"], self.info["frame"]["h"]
         r = self.info["region"]

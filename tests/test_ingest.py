@@ -75,8 +75,14 @@ def test_camera_placement_per_render_case(case):
     w, h = (int(a[a.index("-r") + 1]), int(a[a.index("-r") + 2])) if "-r" in a else (800, 600)
     lr = float(a[a.index("-b") + 1]) if "-b" in a else 0.25
     fd = float(a[a.index("-d") + 1]) if "-d" in a else 4.7
-    name = c["dae"][:-4]
-    _, cam = rrt.load_collada(_input(name), w, h, lr, fd)
+    if c["dae"].startswith("@"):  # generated asset (rrt_scenes.py); the digest is pinned
+        import rrt_scenes
+        import tempfile
+        path = os.path.join(tempfile.mkdtemp(), "gen.dae")
+        assert {"@cfg4": rrt_scenes.write_cfg4_dae}[c["dae"]](path) == c["dae_sha256"]
+    else:
+        path = _input(c["dae"][:-4])
+    _, cam = rrt.load_collada(path, w, h, lr, fd)
     ref = rrt.load_camera_state(os.path.join(GOLD, case, "camera.rrtc"))
     assert bytes(cam) == bytes(ref)
     # and the rrt_set_camera subset agrees with the .rrtc loader's
