@@ -116,6 +116,17 @@ typedef struct {
 /* Replaces: the `-B x y z r dtheta` override of the global black hole (main.cpp:139-145). */
 int rrt_set_spacetime(rrt_ctx* ctx, const rrt_spacetime_desc* st);
 
+/* ---------------------------------------------------------------- environment map */
+typedef struct {
+  uint32_t width, height;     /* equirectangular map, HDRImageBuffer layout: row y covers
+                                 theta = (y + 0.5) / height * pi from +y (environment_light.cpp) */
+  const float* texels;        /* [height][width][3] linear RGB (Spectrum), main.cpp:64-75 order */
+} rrt_envmap_desc;
+/* Replaces: the envmap argument of PathTracer::PathTracer -> EnvironmentLight
+ * (pathtracer.cpp:61-63, environment_light.cpp:21-148): importance-sampled light and the miss
+ * radiance.  The library copies the texels and builds the sampling CDFs.  NULL removes it. */
+int rrt_set_envmap(rrt_ctx* ctx, const rrt_envmap_desc* envmap);
+
 /* ---------------------------------------------------------------- render */
 typedef struct {
   uint32_t ns_aa;             /* -s   (AppConfig default 1) */
@@ -231,6 +242,21 @@ void rrt_scene_file_free(rrt_scene_file* f);
 int rrt_camera_file_load(const char* path, rrt_camera_desc* out);
 /* .rrts writer (the layout rrt_scene_file_load reads). */
 int rrt_scene_file_save(const char* path, const rrt_scene_desc* scene);
+
+/* ---------------------------------------------------------------- image output (host only) */
+/* HDRImageBuffer::toColor + ImageBuffer::update_pixel for one pixel (image.h:53-62, 183-198):
+ * RGBA8 packed R in the low byte. */
+uint32_t rrt_tonemap_pixel(const float rgb[3]);
+/* PNG file of w x h RGBA8 pixels, rows top to bottom (what lodepng::encode writes for
+ * PathTracer::save_image, pathtracer.cpp:646-684). */
+int rrt_write_png(const char* path, const uint32_t* rgba, uint32_t w, uint32_t h);
+
+/* OpenEXR environment maps (main.cpp:42-79 load_exr): single-part scanline files without
+ * compression, HALF or FLOAT channels; R, G, B = the file's channels 2, 1, 0 (main.cpp:69-75).
+ * *texels_out = [h][w][3] floats, released with rrt_exr_free.  rrt_exr_save writes FLOAT B,G,R. */
+int rrt_exr_load(const char* path, float** texels_out, uint32_t* w_out, uint32_t* h_out);
+void rrt_exr_free(float* texels);
+int rrt_exr_save(const char* path, const float* rgb, uint32_t w, uint32_t h);
 
 /* ---------------------------------------------------------------- native scene ingest (host only)
  * The full CGL::Camera record: the fields Camera::dump_settings / load_settings exchange

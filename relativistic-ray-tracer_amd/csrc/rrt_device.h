@@ -630,11 +630,11 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf)
 }
 
 // ------------------------------------------------------------------ lights (light.cpp)
-// LEAN: every light is an area light
+// LEAN: every light is an area or a point light
 template <bool LEAN = false>
 __device__ spec light_sample_L(const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
-  switch (LEAN ? 0u : l.type) {
+  switch (LEAN ? (l.type == 1u ? 1u : 0u) : l.type) {
     case 0: {  // AreaLight::sample_L (light.cpp:80-92): float sqDist, sqrtf, float pdf
       double sx, sy;
       g.grid(sx, sy);

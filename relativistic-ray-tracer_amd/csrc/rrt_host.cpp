@@ -90,7 +90,7 @@ struct rrt_ctx {
   std::vector<uint32_t> leaf;
   uint32_t max_depth = 0;
   bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (qdiv, rrt_device.h)
-  bool lean = false;      // area lights only and no microfacet BSDF (LEAN kernel builds)
+  bool lean = false;      // area/point lights only and no microfacet BSDF (LEAN kernel builds)
   uint32_t grid_res = 128;  // empty-space grid cells along the longest root-box axis (<= 1: none)
   std::vector<uint8_t> grid;
   DGrid hgrid{};           // host copy (k = nullptr)
@@ -593,7 +593,8 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     if (c->plane_eps == 0.0) for (DPlane& pl : planes) pl = DPlane{};  // never cull
   }
   c->lean = true;
-  for (const DLight& l : c->lights) if (l.type != RRT_LIGHT_AREA) c->lean = false;
+  for (const DLight& l : c->lights)
+    if (l.type != RRT_LIGHT_AREA && l.type != RRT_LIGHT_POINT) c->lean = false;
   for (const DBsdf& b : c->bsdfs) if (b.type == RRT_BSDF_MICROFACET) c->lean = false;
   c->has_scene = true;
   if (c->device < 0) return RRT_OK;
@@ -630,6 +631,12 @@ extern "C" int rrt_set_camera(rrt_ctx* c, const rrt_camera_desc* cam) {
   d.bly = -std::tan(cam->vFov * (kPI / 180) / 2);
   c->has_camera = true;
   return RRT_OK;
+}
+
+extern "C" int rrt_set_envmap(rrt_ctx* c, const rrt_envmap_desc* env) {
+  if (!c) return RRT_E_INVALID;
+  if (!env) return RRT_OK;
+  return fail(c, RRT_E_INVALID, "environment maps are not supported by this build yet");
 }
 
 extern "C" int rrt_set_spacetime(rrt_ctx* c, const rrt_spacetime_desc* st) {

@@ -18,7 +18,7 @@ __device__ __forceinline__ bool trace(const KParams& kp, v3 o, v3 d, Isect* is, 
   return query<ANY, COUNT>(kp, o, d, is, cn);
 }
 
-// LEAN: area lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
+// LEAN: area/point lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
 // (same values: make_coord_space is a pure function of the normal) instead of being kept live
 // across the shadow query, which keeps 12 VGPRs out of the traversal loop.
 template <bool COUNT, bool LEAN, bool DEEP>

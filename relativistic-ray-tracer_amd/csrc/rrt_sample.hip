@@ -123,7 +123,7 @@ extern "C" int rrt_prof_read(unsigned long long* out) {  // out: 8 + 3 * 16384
 }
 #endif
 
-// COUNT: per-pixel work counters; LEAN: area lights only, no microfacet BSDF, importance-sampled
+// COUNT: per-pixel work counters; LEAN: area/point lights only, no microfacet BSDF, importance-sampled
 // direct light (the BASELINE scenes); WAVES: register budget (minimum waves per SIMD).
 template <bool COUNT, bool LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* __restrict__ kpp) {

@@ -87,7 +87,8 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load",
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
-           "rrt_camera_state_desc"]
+           "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
+           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save"]
 
 _lib = None
 

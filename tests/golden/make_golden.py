@@ -72,6 +72,9 @@ CASES = {
     "cfg4_knot_4k_s256_crop3": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1880", "1180", "64", "64"], False),
     "cfg4_knot_240x135_s16": ("@cfg4", ["-s", "16", "-r", "240", "135"], True),
 }
+# cases whose reference PNG outputs (save_image + save_sampling_rate_image, via -f) are kept as
+# ref.png / ref_rate.png, for the rrt_render CLI tests
+KEEP_PNG = {"cfg1_spheres_480x360_s8", "bunny_1080p_s64_crop", "spheres_96x72_s8_l4"}
 # generated scenes: "@name" -> writer(path) -> sha256 (the tests regenerate and check the digest)
 sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
 import rrt_scenes  # noqa: E402
@@ -153,6 +156,9 @@ def main():
                                     nodes=np.load(prefix + "_bvh_nodes.npy"),
                                     prims=np.load(prefix + "_bvh_prims.npy"))
             shutil.copy(prefix + ".rrtc", os.path.join(out, "camera.rrtc"))
+            if name in KEEP_PNG:
+                shutil.copy(os.path.join(td, "out.png"), os.path.join(out, "ref.png"))
+                shutil.copy(os.path.join(td, "out_rate.png"), os.path.join(out, "ref_rate.png"))
             px = load_px(prefix, counters)
             np.savez_compressed(os.path.join(out, "px.npz"), **px)
         meta = px["meta"]

@@ -1,0 +1,35 @@
+"""GPU: the reference's command line, end to end (rrt_render = main.cpp's windowless path over
+rrt::PathTracer, the native COLLADA ingest and librrt's HIP kernels).  The PNG and the sampling-
+rate PNG it writes must equal, pixel for pixel, the files the reference itself wrote for the same
+flags (tests/golden/<case>/ref.png, ref_rate.png; make_golden.py KEEP_PNG)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden_cases import GOLD
+from png_util import read_png
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+CLI = os.path.join(ROOT, "relativistic-ray-tracer_amd", "rrt_render")
+
+
+@pytest.mark.parametrize("case", ["spheres_96x72_s8_l4", "cfg1_spheres_480x360_s8", "bunny_1080p_s64_crop"])
+def test_cli_png_matches_reference(case, tmp_path):
+    info = json.load(open(os.path.join(GOLD, case, "case.json")))
+    out = str(tmp_path / "out.png")
+    cmd = [CLI] + info["args"] + ["-f", out, os.path.join(GOLD, "dae", info["dae"])]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    print(r.stdout[-400:], r.stderr[-400:])
+    assert r.returncode == 0
+    assert np.array_equal(read_png(out), read_png(os.path.join(GOLD, case, "ref.png")))
+    assert np.array_equal(read_png(str(tmp_path / "out_rate.png")), read_png(os.path.join(GOLD, case, "ref_rate.png")))
+
+
+def test_cli_usage_and_errors(tmp_path):
+    assert subprocess.run([CLI], capture_output=True).returncode == 1
+    r = subprocess.run([CLI, "-f", str(tmp_path / "x.png"), "/nonexistent.dae"], capture_output=True, text=True)
+    assert r.returncode == 2 and "cannot open" in r.stderr
