@@ -22,6 +22,8 @@
 //   <prefix>_px_*.npy    per-pixel results for the rendered region
 //
 // Extra flags beyond the reference's getopt string: -S <seed>, -O <prefix>, -Q (dump only).
+// -e <file.exr> loads the environment map the way main.cpp:42-79 does (the reference's vendored
+// tinyexr, compiled in harness_exr.cpp) and hands it to the PathTracer constructor.
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -68,6 +70,7 @@ using namespace CGL;
 using CGL::StaticScene::global_black_hole;
 
 namespace harness { thread_local ThreadRng g_rng; }
+HDRImageBuffer* harness_load_exr(const char* path);  // harness_exr.cpp (main.cpp:42-79 re-enacted)
 using harness::g_rng;
 
 // ------------------------------------------------------------------------------------------
@@ -185,7 +188,10 @@ static void dump_scene(const std::string& path, StaticScene::Scene* scene) {
     } else { std::fprintf(stderr, "[harness] unknown object type\n"); std::exit(3); }
   }
   // Light record: u32 type, u32 is_delta, f32 radiance[3], f32 area, f64 v[12]  (120 bytes)
+  uint32_t n_dumped_lights = 0;
   for (StaticScene::SceneLight* l : scene->lights) {
+    if (dynamic_cast<StaticScene::EnvironmentLight*>(l)) continue;  // given separately (-e file)
+    ++n_dumped_lights;
     uint32_t type = 0xffffffffu;
     float rad[3] = {0, 0, 0}, area = 0;
     Vector3D v[4];
@@ -212,7 +218,7 @@ static void dump_scene(const std::string& path, StaticScene::Scene* scene) {
   const char magic[8] = {'R', 'R', 'T', 'S', 'C', 'N', '1', 0};
   out.insert(out.end(), magic, magic + 8);
   put(out, (uint32_t)bsdfs.size()); put(out, (uint32_t)scene->objects.size());
-  put(out, (uint32_t)scene->lights.size()); put(out, (uint32_t)0);
+  put(out, n_dumped_lights); put(out, (uint32_t)0);
   for (BSDF* b : bsdfs) put_bsdf(out, b);
   out.insert(out.end(), objs.begin(), objs.end());
   out.insert(out.end(), lights.begin(), lights.end());
@@ -318,7 +324,10 @@ int main(int argc, char** argv) {
       case 'm': config.pathtracer_max_ray_depth = atoi(optarg); break;
       case 'b': config.pathtracer_lensRadius = atof(optarg); break;
       case 'd': config.pathtracer_focalDistance = atof(optarg); break;
-      case 'e': std::fprintf(stderr, "-e (EXR envmap) not supported by the harness\n"); return 1;
+      case 'e':
+        config.pathtracer_envmap = harness_load_exr(optarg);
+        if (!config.pathtracer_envmap) return 1;
+        break;
       case 'c': cam_settings = optarg; break;
       case 'a':
         config.pathtracer_samples_per_patch = atoi(argv[optind - 1]);
@@ -408,6 +417,20 @@ int main(int argc, char** argv) {
   pt->set_scene(scene->get_static_scene());
   pt->set_frame_size(screenW, screenH);
 
+  if (pt->envLight) {  // EnvironmentLight::init accumulates into new double[h]: must have started at zero
+    StaticScene::EnvironmentLight* el = pt->envLight;
+    const HDRImageBuffer* em = el->envMap;
+    double run = 0;
+    for (size_t j = 0; j < em->h; ++j) {
+      double row = 0;
+      for (size_t i = 0; i < em->w; ++i) row += el->pdf_envmap[em->w * j + i];
+      run = (j > 0) ? row + run : row;
+      if (run != el->marginal_y[j]) {
+        std::fprintf(stderr, "[harness] EnvironmentLight::marginal_y[%zu] was not zero-initialised\n", j);
+        return 6;
+      }
+    }
+  }
   dump_scene(prefix + ".rrts", pt->scene);
   dump_camera(prefix + ".rrtc", pt->camera);
   dump_bvh(prefix, pt->scene, pt->bvh->root);
@@ -416,6 +439,12 @@ int main(int argc, char** argv) {
   g_frame_w = pt->sampleBuffer.w;
   g_frame_h = pt->sampleBuffer.h;
   g_pixels.assign(g_frame_w * g_frame_h, PixelRecord{});
+  // Cell mode (-p) sizes tile_samples for the cell's 8-pixel tiles but raytrace_tile indexes it
+  // by absolute 32-pixel tile coordinates (pathtracer.cpp:256-258 vs :561-579): the increments
+  // land past the end of the vector, corrupting the heap (observed aborts at 4K).  The counts are
+  // never read for the image, so give the vector enough capacity that the reference's own
+  // resize() keeps a buffer the stray increments stay inside.
+  pt->tile_samples.reserve((size_t)1 << 22);
   pt->render_to_file(filename, x, y, dx, dy);
 
   // region actually rendered

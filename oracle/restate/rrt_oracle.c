@@ -144,6 +144,9 @@ struct ro_scene {
   prim_t* prims; uint32_t nprims;
   bsdf_t* bsdfs; uint32_t nbsdfs;
   light_t* lights; uint32_t nlights;
+  /* environment map (ro_scene_set_envmap): texels + EnvironmentLight::init tables */
+  uint32_t env_w, env_h;
+  float* env_tex; double* env_pdf; double* env_conds; double* env_marg;
   node_t* nodes; uint32_t nnodes, cap_nodes;
   uint32_t* leaf; uint32_t nleaf;
 };
@@ -296,6 +299,7 @@ fail:
 void ro_scene_free(ro_scene* s) {
   if (!s) return;
   free(s->pos); free(s->nrm); free(s->prims); free(s->bsdfs); free(s->lights); free(s->nodes); free(s->leaf);
+  free(s->env_tex); free(s->env_pdf); free(s->env_conds); free(s->env_marg);
   free(s);
 }
 int ro_scene_num_prims(const ro_scene* s) { return (int)s->nprims; }
@@ -587,10 +591,92 @@ static spec bsdf_sample_f(const bsdf_t* b, rng_t* g, v3 wo, v3* wi, float* pdf) 
   }
 }
 
+/* ------------------------------------------------------------------ environment light
+ * environment_light.cpp:21-148 (ENV_HEMI == 0).  Spectrum * double narrows the weight to float. */
+static spec env_texel(const ro_scene* s, size_t i) { return S(s->env_tex[3 * i], s->env_tex[3 * i + 1], s->env_tex[3 * i + 2]); }
+static spec env_bilerp(const ro_scene* s, double xx, double yy) { /* :112-127 */
+  long right = lround(xx), left, v = lround(yy);
+  double u1 = right - xx + .5, v1;
+  if (right == 0 || right == (long)s->env_w) { left = (long)s->env_w - 1; right = 0; }
+  else left = right - 1;
+  if (v == 0) { v = 1; v1 = 1; }
+  else if (v == (long)s->env_h) { v = (long)s->env_h - 1; v1 = 0; }
+  else v1 = v - yy + .5;
+  size_t bottom = (size_t)s->env_w * (size_t)v, top = bottom - s->env_w;
+  double u0 = 1 - u1;
+  float fu1 = (float)u1, fu0 = (float)u0, fv1 = (float)v1, fv0 = (float)(1 - v1);
+  spec a = sadd(smulf(env_texel(s, top + left), fu1), smulf(env_texel(s, top + right), fu0));
+  spec b = sadd(smulf(env_texel(s, bottom + left), fu1), smulf(env_texel(s, bottom + right), fu0));
+  return sadd(smulf(a, fv1), smulf(b, fv0));
+}
+static spec env_dir(const ro_scene* s, v3 d) { /* sample_dir :146-148 */
+  v3 u = vunit(d);
+  double theta = acos(u.y), phi = atan2(-u.z, u.x) + PI_D;
+  double x = phi / 2. / PI_D * s->env_w, y = theta / PI_D * s->env_h;
+  return env_bilerp(s, x, y);
+}
+static uint32_t upper_bound_d(const double* a, uint32_t n, double value) { /* std::upper_bound */
+  uint32_t first = 0, count = n;
+  while (count > 0) {
+    uint32_t step = count >> 1, it = first + step;
+    if (!(value < a[it])) { first = it + 1; count -= step + 1; }
+    else count = step;
+  }
+  return first;
+}
+static spec env_sample(const ro_scene* s, rng_t* g, v3* wi, float* dist, float* pdf) { /* :130-144 */
+  *dist = INFINITY;
+  double sx, sy;
+  grid_sample(g, &sx, &sy);
+  uint32_t y = upper_bound_d(s->env_marg, s->env_h, sy);
+  if (y >= s->env_h) y = s->env_h - 1;  /* (the reference reads one row past the table) */
+  uint32_t x = upper_bound_d(s->env_conds + (size_t)s->env_w * y, s->env_w, sx);
+  if (x >= s->env_w) x = s->env_w - 1;
+  double phi = (double)x / s->env_w * 2.0 * PI_D, theta = (double)y / s->env_h * PI_D;
+  *wi = V(cos(phi - PI_D) * sin(theta), cos(theta), -sin(phi - PI_D) * sin(theta));
+  *pdf = (float)(s->env_pdf[(size_t)s->env_w * y + x] * s->env_w * s->env_h / (2 * M_PI * M_PI * sin(theta)));
+  return env_bilerp(s, (double)x, (double)y);
+}
+
+int ro_scene_set_envmap(ro_scene* s, uint32_t w, uint32_t h, const float* texels) {
+  if (!s || !texels || !w || !h || s->env_w) return -1;
+  s->env_tex = (float*)malloc(sizeof(float) * 3 * (size_t)w * h);
+  s->env_pdf = (double*)calloc((size_t)w * h, sizeof(double));
+  s->env_conds = (double*)calloc((size_t)w * h, sizeof(double));
+  s->env_marg = (double*)calloc(h, sizeof(double));
+  memcpy(s->env_tex, texels, sizeof(float) * 3 * (size_t)w * h);
+  double sum = 0;  /* EnvironmentLight::init :21-45 */
+  for (uint32_t j = 0; j < h; ++j)
+    for (uint32_t i = 0; i < w; ++i) {
+      const float* t = &s->env_tex[3 * ((size_t)w * j + i)];
+      float il = 0.2126f * t[0] + 0.7152f * t[1] + 0.0722f * t[2];
+      s->env_pdf[(size_t)w * j + i] = il * sin(PI_D * (j + .5) / h);
+      sum += s->env_pdf[(size_t)w * j + i];
+    }
+  for (uint32_t j = 0; j < h; ++j) {
+    for (uint32_t i = 0; i < w; ++i) s->env_marg[j] += (s->env_pdf[(size_t)w * j + i] /= sum);
+    for (uint32_t i = 0; i < w; ++i) {
+      s->env_conds[(size_t)w * j + i] = s->env_pdf[(size_t)w * j + i] / s->env_marg[j];
+      if (i > 0) s->env_conds[(size_t)w * j + i] += s->env_conds[(size_t)w * j + i - 1];
+    }
+    if (j > 0) s->env_marg[j] += s->env_marg[j - 1];
+  }
+  s->env_w = w; s->env_h = h;
+  /* PathTracer::set_scene appends envLight after the scene's lights (pathtracer.cpp:106-108) */
+  s->lights = (light_t*)realloc(s->lights, sizeof(light_t) * (s->nlights + 1));
+  memset(&s->lights[s->nlights], 0, sizeof(light_t));
+  s->lights[s->nlights].type = 5;
+  s->lights[s->nlights].is_delta = 0;
+  s->nlights++;
+  return 0;
+}
+
 /* ------------------------------------------------------------------ lights (light.cpp) */
-static spec light_sample_L(const light_t* l, rng_t* g, v3 p, v3* wi, float* dist, float* pdf) {
+static spec light_sample_L(const ro_scene* s, const light_t* l, rng_t* g, v3 p, v3* wi, float* dist, float* pdf) {
   spec rad = S(l->rad[0], l->rad[1], l->rad[2]);
   switch (l->type) {
+    case 5: /* EnvironmentLight */
+      return env_sample(s, g, wi, dist, pdf);
     case 0: { /* AreaLight::sample_L, light.cpp:80-92 */
       double sx, sy;
       grid_sample(g, &sx, &sy);
@@ -657,7 +743,7 @@ static spec direct_importance(pctx* c, const isect_t* is) { /* :33-57 */
     total += num;
     for (int i = 0; i < num; ++i) {
       v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L(l, c->q.g, hit_p, &wi_world, &dist, &pdf);
+      spec sample = light_sample_L(c->q.s, l, c->q.g, hit_p, &wi_world, &dist, &pdf);
       v3 w_in = to_local(X, Y, Z, wi_world);
       if (w_in.z < 0) continue;
       if (!bvh_intersect(&c->q, vadd(hit_p, smul(EPS_D, wi_world)), wi_world, NULL))
@@ -695,7 +781,8 @@ static spec at_least_one_bounce(pctx* c, uint32_t depth, const isect_t* is) { /*
 
 static spec est_radiance(pctx* c, v3 o, v3 d) { /* :103-123, ILLUM == 2 */
   isect_t is;
-  if (!bvh_intersect(&c->q, o, d, &is)) return S(0, 0, 0); /* no envLight */
+  if (!bvh_intersect(&c->q, o, d, &is)) /* miss: envLight->sample_dir(r), r unbent */
+    return c->q.s->env_w ? env_dir(c->q.s, d) : S(0, 0, 0);
   spec e = bsdf_emission(&c->q.s->bsdfs[is.bsdf]);
   if (c->p->max_ray_depth == 0) return e;
   if (c->p->max_ray_depth == 1) return sadd(e, one_bounce(c, &is));
@@ -893,7 +980,7 @@ void ro_area_sample(const float* rad, const double* v, const double* p, const in
   l.area = (float)(vnorm(l.v[2]) * vnorm(l.v[3])); /* light.cpp:78 */
   rng_t g; memset(&g, 0, sizeof(g)); g.script = rands; g.script_len = 2;
   v3 w;
-  spec s = light_sample_L(&l, &g, V(p[0], p[1], p[2]), &w, dist, pdf);
+  spec s = light_sample_L(NULL, &l, &g, V(p[0], p[1], p[2]), &w, dist, pdf);
   L[0] = s.r; L[1] = s.g; L[2] = s.b; wi[0] = w.x; wi[1] = w.y; wi[2] = w.z;
 }
 void ro_camera_ray(double hFov, double vFov, const double* pos, const double* c2w, double nClip, double fClip,

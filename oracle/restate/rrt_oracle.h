@@ -30,6 +30,9 @@ int ro_scene_num_nodes(const ro_scene* s);
 /* BVH in left-first pre-order: boxes [n][6] (min, max), nodes [n][4] (first, count, left,
  * right), prims [n_prims] (build-order primitive ids) -- same layout as the oracle dump. */
 void ro_scene_bvh(const ro_scene* s, double* boxes, int32_t* nodes, uint32_t* prims);
+/* Attach an environment map ([h][w][3] RGB, HDRImageBuffer layout): EnvironmentLight::init's
+ * tables, and the light appended after the scene's lights (pathtracer.cpp:61-63, 106-108). */
+int ro_scene_set_envmap(ro_scene* s, uint32_t w, uint32_t h, const float* texels);
 
 typedef struct {
   double hFov, vFov, nClip, fClip;

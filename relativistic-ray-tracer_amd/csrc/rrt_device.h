@@ -629,10 +629,62 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf)
   }
 }
 
+// ------------------------------------------------------------------ environment light
+// environment_light.cpp:89-148.  Texel arithmetic in float (Spectrum * double narrows the
+// weight to float, as Spectrum::operator*(float) does).
+__device__ __forceinline__ spec env_texel(const DEnv& e, size_t i) {
+  return S(e.tex[3 * i], e.tex[3 * i + 1], e.tex[3 * i + 2]);
+}
+__device__ spec env_bilerp(const DEnv& e, double xx, double yy) {  // :112-127
+  long right = lround(xx), left, v = lround(yy);
+  double u1 = right - xx + .5, v1;
+  if (right == 0 || right == (long)e.w) { left = (long)e.w - 1; right = 0; }
+  else left = right - 1;
+  if (v == 0) { v = 1; v1 = 1; }
+  else if (v == (long)e.h) { v = (long)e.h - 1; v1 = 0; }
+  else v1 = v - yy + .5;
+  const size_t bottom = (size_t)e.w * (size_t)v, top = bottom - e.w;
+  const double u0 = 1 - u1;
+  const float fu1 = (float)u1, fu0 = (float)u0, fv1 = (float)v1, fv0 = (float)(1 - v1);
+  return ((env_texel(e, top + left) * fu1) + (env_texel(e, top + right) * fu0)) * fv1 +
+         ((env_texel(e, bottom + left) * fu1) + (env_texel(e, bottom + right) * fu0)) * fv0;
+}
+// sample_dir (:146-148): radiance seen along direction d (the unbent camera ray on a miss)
+__device__ spec env_dir(const DEnv& e, v3 d) {
+  const v3 u = unit(d);
+  const double theta = acos(u.y), phi = atan2(-u.z, u.x) + PI_D;  // dir_to_theta_phi (:89-94)
+  const double x = phi / 2. / PI_D * e.w, y = theta / PI_D * e.h;  // theta_phi_to_xy (:71-77)
+  return env_bilerp(e, x, y);
+}
+// std::upper_bound over a double array (libstdc++'s halving loop, value < *it)
+__device__ __forceinline__ uint32_t upper_bound_d(const double* a, uint32_t n, double value) {
+  uint32_t first = 0, count = n;
+  while (count > 0) {
+    const uint32_t step = count >> 1, it = first + step;
+    if (!(value < a[it])) { first = it + 1; count -= step + 1; }
+    else count = step;
+  }
+  return first;
+}
+// sample_L (:130-144, ENV_HEMI == 0): row by the marginal CDF, column by the row's conditional CDF
+__device__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float& dist, float& pdf) {
+  dist = INFINITY;
+  double sx, sy;
+  g.grid(sx, sy);
+  uint32_t y = upper_bound_d(e.marg, e.h, sy);
+  if (y >= e.h) y = e.h - 1;  // (the reference reads one row past the table when sy == 1)
+  uint32_t x = upper_bound_d(e.conds + (size_t)e.w * y, e.w, sx);
+  if (x >= e.w) x = e.w - 1;
+  const double phi = (double)x / e.w * 2.0 * PI_D, theta = (double)y / e.h * PI_D;  // xy_to_theta_phi
+  wi = V(cos(phi - PI_D) * sin(theta), cos(theta), -sin(phi - PI_D) * sin(theta));  // theta_phi_to_dir
+  pdf = (float)(e.pdf[(size_t)e.w * y + x] * e.w * e.h / (2 * PI_D * PI_D * sin(theta)));
+  return env_bilerp(e, (double)x, (double)y);
+}
+
 // ------------------------------------------------------------------ lights (light.cpp)
 // LEAN: every light is an area or a point light
 template <bool LEAN = false>
-__device__ spec light_sample_L(const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
+__device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
   switch (LEAN ? (l.type == 1u ? 1u : 0u) : l.type) {
     case 0: {  // AreaLight::sample_L (light.cpp:80-92): float sqDist, sqrtf, float pdf
@@ -656,6 +708,8 @@ __device__ spec light_sample_L(const DLight& l, Rng& g, v3 p, v3& wi, float& dis
     case 2:  // DirectionalLight
       wi = ld3(l.v[0]); dist = INFINITY; pdf = 1.0f;
       return rad;
+    case 5:  // EnvironmentLight (appended by PathTracer::set_scene, pathtracer.cpp:106-108)
+      return env_sample(env, g, wi, dist, pdf);
     default: {  // InfiniteHemisphereLight
       v3 dir = hemisphere_sample(g);
       Frame f; f.X = ld3(l.v[0]); f.Y = ld3(l.v[1]); f.Z = ld3(l.v[2]);

@@ -95,7 +95,15 @@ struct rrt_ctx {
   std::vector<uint8_t> grid;
   DGrid hgrid{};           // host copy (k = nullptr)
   std::vector<DBsdf> bsdfs;
-  std::vector<DLight> lights;
+  std::vector<DLight> lights;  // the scene's lights (the environment light is appended on upload)
+  // environment map (rrt_set_envmap): texels and EnvironmentLight::init's tables, host + device
+  uint32_t env_w = 0, env_h = 0;
+  std::vector<float> env_tex;
+  std::vector<double> env_pdf, env_conds, env_marg;
+  float* d_env_tex = nullptr;
+  double* d_env_pdf = nullptr;
+  double* d_env_conds = nullptr;
+  double* d_env_marg = nullptr;
   bool has_scene = false, has_camera = false;
   DCamera cam{};
   DHole hole{};
@@ -145,6 +153,12 @@ static int fail(rrt_ctx* c, int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(c, RRT_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+static void free_env_dev(rrt_ctx* c) {
+  if (c->device < 0) return;
+  hipFree(c->d_env_tex); hipFree(c->d_env_pdf); hipFree(c->d_env_conds); hipFree(c->d_env_marg);
+  c->d_env_tex = nullptr; c->d_env_pdf = nullptr; c->d_env_conds = nullptr; c->d_env_marg = nullptr;
+}
+
 static void free_scene_dev(rrt_ctx* c) {
   if (c->device < 0) return;
   hipFree(c->d_nodes); hipFree(c->d_geo); hipFree(c->d_nrm); hipFree(c->d_meta); hipFree(c->d_bsdfs);
@@ -190,6 +204,7 @@ void rrt_destroy(rrt_ctx* c) {
   if (c->device >= 0) {
     hipSetDevice(c->device);
     free_scene_dev(c);
+    free_env_dev(c);
     hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -453,10 +468,30 @@ static int upload(rrt_ctx* c, void** dst, const void* src, size_t bytes) {
   return RRT_OK;
 }
 
+// The light table the kernels see: the scene's lights, then the environment light if any
+// (PathTracer::set_scene pushes envLight after the scene's lights, pathtracer.cpp:106-108).
+static std::vector<DLight> all_lights(const rrt_ctx* c) {
+  std::vector<DLight> l = c->lights;
+  if (c->env_w) {
+    DLight e{};
+    e.type = 5; e.is_delta = 0;  // EnvironmentLight::is_delta_light() == false
+    l.push_back(e);
+  }
+  return l;
+}
+static int upload_lights(rrt_ctx* c) {
+  if (c->device < 0) return RRT_OK;
+  hipFree(c->d_lights);
+  c->d_lights = nullptr;
+  const std::vector<DLight> l = all_lights(c);
+  if (l.empty()) return RRT_OK;
+  return upload(c, (void**)&c->d_lights, l.data(), l.size() * sizeof(DLight));
+}
+
 extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if (!c || !s) return fail(c, RRT_E_INVALID, "null argument");
   if (s->n_bsdfs > RRT_MAX_BSDFS) return fail(c, RRT_E_INVALID, "too many BSDFs (max 64)");
-  if (s->n_lights > RRT_MAX_LIGHTS) return fail(c, RRT_E_INVALID, "too many lights (max 16)");
+  if (s->n_lights + 1 > RRT_MAX_LIGHTS) return fail(c, RRT_E_INVALID, "too many lights (max 15 + environment)");
   if (s->n_objects && !s->objects) return fail(c, RRT_E_INVALID, "objects missing");
   if (s->n_bsdfs && !s->bsdfs) return fail(c, RRT_E_INVALID, "bsdfs missing");
   if (s->n_lights && !s->lights) return fail(c, RRT_E_INVALID, "lights missing");
@@ -472,7 +507,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     const rrt_light_desc& L = s->lights[i];
     if (L.type > RRT_LIGHT_HEMISPHERE)
       return fail(c, RRT_E_INVALID, "unsupported light type (spot/sphere/mesh lights are stubs in the reference; "
-                                    "environment maps are not implemented yet)");
+                                    "an environment map is given with rrt_set_envmap)");
     DLight& d = c->lights[i];
     d.type = L.type; d.is_delta = L.is_delta;
     std::memcpy(d.rad, L.radiance, sizeof(d.rad)); d.area = L.area;
@@ -606,7 +641,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if ((rc = upload(c, (void**)&c->d_nrm, nrm.data(), nrm.size() * sizeof(DPrimNrm)))) return rc;
   if ((rc = upload(c, (void**)&c->d_meta, meta.data(), meta.size() * sizeof(DPrimMeta)))) return rc;
   if ((rc = upload(c, (void**)&c->d_bsdfs, c->bsdfs.data(), c->bsdfs.size() * sizeof(DBsdf)))) return rc;
-  if ((rc = upload(c, (void**)&c->d_lights, c->lights.data(), c->lights.size() * sizeof(DLight)))) return rc;
+  if ((rc = upload_lights(c))) return rc;
   if (!c->grid.empty() && (rc = upload(c, (void**)&c->d_grid, c->grid.data(), c->grid.size()))) return rc;
   if ((rc = upload(c, (void**)&c->d_planes, planes.data(), planes.size() * sizeof(DPlane)))) return rc;
   if (c->has_clean) {
@@ -633,10 +668,53 @@ extern "C" int rrt_set_camera(rrt_ctx* c, const rrt_camera_desc* cam) {
   return RRT_OK;
 }
 
+// EnvironmentLight::init (environment_light.cpp:21-45): pdf = illum * sin(theta_j), normalised;
+// per-row conditional CDFs; marginal CDF over rows (marginal_y starts at zero -- the reference
+// reads an uninitialised array here).  Same loop and summation order, host libm.
 extern "C" int rrt_set_envmap(rrt_ctx* c, const rrt_envmap_desc* env) {
   if (!c) return RRT_E_INVALID;
-  if (!env) return RRT_OK;
-  return fail(c, RRT_E_INVALID, "environment maps are not supported by this build yet");
+  free_env_dev(c);
+  c->env_w = c->env_h = 0;
+  c->env_tex.clear(); c->env_pdf.clear(); c->env_conds.clear(); c->env_marg.clear();
+  if (env) {
+    if (!env->texels || env->width == 0 || env->height == 0) return fail(c, RRT_E_INVALID, "empty environment map");
+    if ((uint64_t)env->width * env->height > (1ull << 28)) return fail(c, RRT_E_INVALID, "environment map too large");
+    const uint32_t w = env->width, h = env->height;
+    c->env_tex.assign(env->texels, env->texels + (size_t)w * h * 3);
+    c->env_pdf.assign((size_t)w * h, 0.0);
+    c->env_conds.assign((size_t)w * h, 0.0);
+    c->env_marg.assign(h, 0.0);
+    double sum = 0;
+    for (uint32_t j = 0; j < h; ++j)
+      for (uint32_t i = 0; i < w; ++i) {
+        const float* t = &c->env_tex[3 * ((size_t)w * j + i)];
+        const float illum = 0.2126f * t[0] + 0.7152f * t[1] + 0.0722f * t[2];  // Spectrum::illum
+        c->env_pdf[(size_t)w * j + i] = illum * std::sin(kPI * (j + .5) / h);
+        sum += c->env_pdf[(size_t)w * j + i];
+      }
+    for (uint32_t j = 0; j < h; ++j) {
+      for (uint32_t i = 0; i < w; ++i) c->env_marg[j] += (c->env_pdf[(size_t)w * j + i] /= sum);
+      for (uint32_t i = 0; i < w; ++i) {
+        c->env_conds[(size_t)w * j + i] = c->env_pdf[(size_t)w * j + i] / c->env_marg[j];
+        if (i > 0) c->env_conds[(size_t)w * j + i] += c->env_conds[(size_t)w * j + i - 1];
+      }
+      if (j > 0) c->env_marg[j] += c->env_marg[j - 1];
+    }
+    c->env_w = w; c->env_h = h;
+    if (c->device >= 0) {
+      HIPCHK(c, hipSetDevice(c->device));
+      int rc;
+      if ((rc = upload(c, (void**)&c->d_env_tex, c->env_tex.data(), c->env_tex.size() * sizeof(float)))) return rc;
+      if ((rc = upload(c, (void**)&c->d_env_pdf, c->env_pdf.data(), c->env_pdf.size() * sizeof(double)))) return rc;
+      if ((rc = upload(c, (void**)&c->d_env_conds, c->env_conds.data(), c->env_conds.size() * sizeof(double)))) return rc;
+      if ((rc = upload(c, (void**)&c->d_env_marg, c->env_marg.data(), c->env_marg.size() * sizeof(double)))) return rc;
+    }
+  }
+  if (c->has_scene) {
+    if (c->lights.size() + (c->env_w ? 1 : 0) > RRT_MAX_LIGHTS) return fail(c, RRT_E_INVALID, "too many lights");
+    return upload_lights(c);
+  }
+  return RRT_OK;
 }
 
 extern "C" int rrt_set_spacetime(rrt_ctx* c, const rrt_spacetime_desc* st) {
@@ -698,7 +776,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 64, stream));
   KParams kp{};
   kp.nodes = c->d_nodes; kp.geo = c->d_geo; kp.nrm = c->d_nrm; kp.meta = c->d_meta;
-  kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size();
+  kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size() + (c->env_w ? 1u : 0u);
+  kp.env.tex = c->d_env_tex; kp.env.pdf = c->d_env_pdf; kp.env.conds = c->d_env_conds; kp.env.marg = c->d_env_marg;
+  kp.env.w = c->env_w; kp.env.h = c->env_h;
   kp.fast_div = (c->fast_div && !(p->flags & RRT_RENDER_EXACT_DIV)) ? 1u : 0u;
   kp.cam = c->cam; kp.hole = c->hole;
   kp.grid = c->hgrid;
@@ -739,7 +819,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
   const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
   const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
-  const int lean = (!deep && !count && c->lean && !p->direct_hemisphere) ? 1 : 0;
+  const int lean = (!deep && !count && c->lean && !c->env_w && !p->direct_hemisphere) ? 1 : 0;
+  if (mega && c->env_w) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel has no environment-map path");
   const uint32_t wv = p->variant & 0xffu;
   const int waves = (wv >= 1 && wv <= 6) ? (int)wv : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
@@ -755,11 +836,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     uint32_t dh = 2;
     if (p->max_ray_depth >= 1) {
       if (p->direct_hemisphere) {
-        dh += 2u * (uint32_t)c->lights.size() * p->ns_area_light;
+        dh += 2u * (uint32_t)all_lights(c).size() * p->ns_area_light;
       } else {
-        for (const DLight& l : c->lights) {
+        for (const DLight& l : all_lights(c)) {
           const uint32_t num = l.is_delta ? 1u : p->ns_area_light;
-          const bool sampled = l.type == RRT_LIGHT_AREA || l.type == RRT_LIGHT_HEMISPHERE;  // 2 draws each
+          // area, hemisphere and environment samplers draw 2 each; point / directional none
+          const bool sampled = l.type == RRT_LIGHT_AREA || l.type == RRT_LIGHT_HEMISPHERE || l.type == 5u;
           dh += sampled ? 2u * num : 0u;
         }
       }

@@ -52,6 +52,17 @@ struct DLight {
   double v[4][3];
 };
 
+// Environment light (EnvironmentLight, environment_light.cpp:21-148): texels and the sampling
+// tables the reference builds in init() (pdf, per-row conditional CDFs, marginal CDF), all on
+// the host with the reference's arithmetic.  w == 0: no environment map.
+struct DEnv {
+  const float* tex;      // [h][w][3] Spectrum
+  const double* pdf;     // [h][w] normalised pdf_envmap
+  const double* conds;   // [h][w] conds_y
+  const double* marg;    // [h]    marginal_y
+  uint32_t w, h;
+};
+
 struct DCamera {
   double pos[3];
   double c2w0[3], c2w1[3], c2w2[3];   // columns
@@ -99,6 +110,7 @@ struct KParams {
   uint32_t n_big;
   DCamera cam;
   DHole hole;
+  DEnv env;
   // render
   uint32_t ns_aa, max_ray_depth, ns_area_light, samples_per_batch;
   float max_tolerance;

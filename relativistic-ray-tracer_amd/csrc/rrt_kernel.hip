@@ -32,7 +32,7 @@ __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Co
     total += num;
     for (int i = 0; i < num; ++i) {
       v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L<LEAN>(l, g, is.hit_p, wi_world, dist, pdf);
+      spec sample = light_sample_L<LEAN>(kp.env, l, g, is.hit_p, wi_world, dist, pdf);
       const Frame f = coord_space(is.n);
       v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
@@ -118,7 +118,8 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
 template <bool DEEP, bool COUNT, bool LEAN>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
-  if (!trace<false, COUNT, DEEP>(kp, o, d, &is, cn)) return S(0, 0, 0);
+  if (!trace<false, COUNT, DEEP>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
+    return (!LEAN && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
   if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_mega_kernel(const KParams* __r
             if (lk >= num) { ++li; lk = 0; continue; }
             ++lk;
             v3 wi; float dist, pdf;
-            const spec smp = light_sample_L(l, g, hp, wi, dist, pdf);
+            const spec smp = light_sample_L(kp.env, l, g, hp, wi, dist, pdf);
             const Frame f = coord_space(nn);
             const v3 w_in = to_local(f, wi);
             if (w_in.z < 0) continue;

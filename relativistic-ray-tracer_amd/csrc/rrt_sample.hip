@@ -59,7 +59,7 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl
       const v3 nn = V(lget(cl.nn[0], t), lget(cl.nn[1], t), lget(cl.nn[2], t));
       const v3 wo = V(lget(cl.wo[0], t), lget(cl.wo[1], t), lget(cl.wo[2], t));
       v3 wi_world; float dist, pdf;
-      const spec sample = light_sample_L<LEAN>(kp.lights[li], g, hp, wi_world, dist, pdf);
+      const spec sample = light_sample_L<LEAN>(kp.env, kp.lights[li], g, hp, wi_world, dist, pdf);
       const Frame f = coord_space(nn);
       const v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
@@ -218,6 +218,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         else if (LEAN) s = e + direct_importance_lds<COUNT, true>(kp, g, is, cl, t, cn);
         else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<COUNT>(kp, g, is, cl, t, cn);
         else s = e + direct_importance_lds<COUNT, false>(kp, g, is, cl, t, cn);
+      } else if (!LEAN && kp.env.w) {
+        s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
       }
     }
     const spec ret = S(lget(cl.rr, t), lget(cl.rg, t), lget(cl.rb, t)) + s;
@@ -408,6 +410,15 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
     // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
     spec s = S(0, 0, 0);
+    if (!LEAN && act && !hit && kp.env.w) {  // miss: envLight->sample_dir of the unbent camera ray
+      Rng g; g.key = lget(gs.key, gid); g.ctr = off;  // re-derive the ray from its jitter draws
+      double jx, jy; g.grid(jx, jy);
+      const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
+      const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
+      const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+      const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+      s = env_dir(kp.env, unit(w));
+    }
     if (act && hit) {
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
@@ -510,6 +521,7 @@ __global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __rest
     Isect is;
     const bool hit = query<false, false>(kp, ld3(cam.pos), unit(w), &is, cn);
     spec s = S(0, 0, 0);
+    if (!hit && !LEAN && kp.env.w) s = env_dir(kp.env, unit(w));
     if (hit) {
       park_hit(cl, t, is);
       g.ctr = kp.draws_miss;

@@ -60,6 +60,10 @@ class ColladaOptions(C.Structure):
                 ("focal_distance", C.c_double), ("reserved", C.c_uint32 * 4)]
 
 
+class EnvmapDesc(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("texels", C.c_void_p)]
+
+
 class SpacetimeDesc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("center", C.c_double * 3), ("r_s", C.c_double),
                 ("delta_theta", C.c_double)]
@@ -108,6 +112,11 @@ def lib():
         L.rrt_set_scene.argtypes = [vp, vp]
         L.rrt_set_camera.argtypes = [vp, C.POINTER(CameraDesc)]
         L.rrt_set_spacetime.argtypes = [vp, C.POINTER(SpacetimeDesc)]
+        if hasattr(L, "rrt_set_envmap"):
+            L.rrt_set_envmap.argtypes = [vp, C.POINTER(EnvmapDesc)]
+            L.rrt_exr_load.argtypes = [C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_uint32),
+                                       C.POINTER(C.c_uint32)]
+            L.rrt_exr_free.argtypes = [vp]
         L.rrt_render_params_default.argtypes = [C.POINTER(RenderParams)]
         L.rrt_render.argtypes = [vp, C.POINTER(RenderParams), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp,
                                  vp, vp, vp]
@@ -220,6 +229,18 @@ def load_camera(path):
     return cam
 
 
+def load_exr(path):
+    """Environment map texels [h][w][3] float32 (rrt_exr_load: main.cpp's load_exr)."""
+    t = C.POINTER(C.c_float)()
+    w, h = C.c_uint32(), C.c_uint32()
+    rc = lib().rrt_exr_load(path.encode(), C.byref(t), C.byref(w), C.byref(h))
+    if rc != RRT_OK:
+        raise RRTError(rc, f"cannot load {path}")
+    arr = np.ctypeslib.as_array(t, shape=(h.value, w.value, 3)).copy()
+    lib().rrt_exr_free(t)
+    return arr
+
+
 def render_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
                   max_tolerance=0.05, direct_hemisphere=False, seed=0, flags=0, variant=0):
     p = RenderParams()
@@ -277,6 +298,16 @@ class Renderer:
         st.center[0], st.center[1], st.center[2] = center
         st.r_s, st.delta_theta = r_s, delta_theta
         self._chk(lib().rrt_set_spacetime(self.h, C.byref(st)))
+
+    def set_envmap(self, texels):
+        """Environment map ([h][w][3] float32) or None (the PathTracer ctor's envmap argument)."""
+        if texels is None:
+            self._chk(lib().rrt_set_envmap(self.h, None))
+            return
+        t = np.ascontiguousarray(texels, np.float32)
+        d = EnvmapDesc()
+        d.width, d.height, d.texels = t.shape[1], t.shape[0], t.ctypes.data
+        self._chk(lib().rrt_set_envmap(self.h, C.byref(d)))
 
     def render(self, params, x0, y0, w, h, draws=False, counters=False):
         rgb = np.zeros((h, w, 3), np.float32)

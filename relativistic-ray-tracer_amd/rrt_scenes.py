@@ -109,3 +109,63 @@ def write_cfg4_dae(path, segments=1000, sides=50):
     with open(path, "wb") as f:
         f.write(text)
     return hashlib.sha256(text).hexdigest()
+
+
+# ------------------------------------------------------------------------------------------
+# cfg5 (BASELINE.json configs[4]): HDR environment map.  SURVEY.md 8(d): a synthetic 1024x512
+# equirectangular f32 RGB map -- analytic sky gradient plus a sun disc, no randomness -- passed
+# with `-e`.  Texel (x, y) covers the direction EnvironmentLight::theta_phi_to_dir gives for
+# theta = (y + 0.5) / h * pi, phi = (x + 0.5) / w * 2 pi (environment_light.cpp:96-106).
+SUN_DIR = np.array([0.45, 0.62, -0.64]) / np.linalg.norm([0.45, 0.62, -0.64])
+
+
+def sky_texels(w=1024, h=512):
+    """[h][w][3] float32 radiance: zenith-to-horizon blue gradient, a warm horizon band, a dark
+    ground below the horizon and a 3-degree sun disc of radiance 60."""
+    theta = (np.arange(h, dtype=np.float64) + 0.5) / h * np.pi
+    phi = (np.arange(w, dtype=np.float64) + 0.5) / w * 2 * np.pi
+    T, P = np.meshgrid(theta, phi, indexing="ij")
+    d = np.stack([np.cos(P - np.pi) * np.sin(T), np.cos(T), -np.sin(P - np.pi) * np.sin(T)], -1)
+    up = d[..., 1]
+    zen = np.array([0.25, 0.45, 1.10])
+    hor = np.array([1.00, 0.85, 0.70])
+    ground = np.array([0.12, 0.10, 0.08])
+    a = np.clip(up, 0.0, 1.0)[..., None]
+    sky = hor * (1 - a) ** 3 + zen * (1 - (1 - a) ** 3)
+    img = np.where(up[..., None] >= 0, sky, ground * (0.6 + 0.4 * np.exp(up[..., None] * 4)))
+    cosang = d @ SUN_DIR
+    sun = cosang > np.cos(np.radians(3.0))
+    img = np.where(sun[..., None], np.array([60.0, 55.0, 45.0]), img)
+    return np.ascontiguousarray(img.astype(np.float32))
+
+
+def write_exr(path, rgb):
+    """Single-part scanline OpenEXR, no compression, FLOAT channels B, G, R (what the reference's
+    tinyexr and rrt_exr_load both read).  Returns the file's SHA-256."""
+    import struct
+    h, w, _ = rgb.shape
+
+    def attr(name, typ, val):
+        return name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<i", len(val)) + val
+    ch = b"".join(n + b"\0" + struct.pack("<iB3xii", 2, 0, 1, 1) for n in (b"B", b"G", b"R")) + b"\0"
+    box = struct.pack("<4i", 0, 0, w - 1, h - 1)
+    hdr = (struct.pack("<II", 20000630, 2) + attr("channels", "chlist", ch) + attr("compression", "compression", b"\0")
+           + attr("dataWindow", "box2i", box) + attr("displayWindow", "box2i", box)
+           + attr("lineOrder", "lineOrder", b"\0") + attr("pixelAspectRatio", "float", struct.pack("<f", 1.0))
+           + attr("screenWindowCenter", "v2f", b"\0" * 8) + attr("screenWindowWidth", "float", struct.pack("<f", 1.0))
+           + b"\0")
+    row_bytes = w * 12
+    base = len(hdr) + 8 * h
+    table = b"".join(struct.pack("<Q", base + y * (8 + row_bytes)) for y in range(h))
+    rows = []
+    for y in range(h):
+        rows.append(struct.pack("<ii", y, row_bytes) + rgb[y, :, 2].tobytes() + rgb[y, :, 1].tobytes()
+                    + rgb[y, :, 0].tobytes())
+    data = hdr + table + b"".join(rows)
+    with open(path, "wb") as f:
+        f.write(data)
+    return hashlib.sha256(data).hexdigest()
+
+
+def write_cfg5_envmap(path, w=1024, h=512):
+    return write_exr(path, sky_texels(w, h))

@@ -71,6 +71,19 @@ CASES = {
     "cfg4_knot_4k_s256_crop2": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1920", "990", "64", "64"], False),
     "cfg4_knot_4k_s256_crop3": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1880", "1180", "64", "64"], False),
     "cfg4_knot_240x135_s16": ("@cfg4", ["-s", "16", "-r", "240", "135"], True),
+    # cfg5 (BASELINE configs[4]) lighting: the generated HDR sky (rrt_scenes.sky_texels, "-e @sky"):
+    # miss radiance of the unbent camera ray + importance-sampled environment light.  The
+    # reference has no Kerr metric, so these pin the environment map under Schwarzschild.
+    "cfg5_bunny_env_4k_s1024_crop": ("CBbunny.dae", ["-s", "1024", "-r", "3840", "2160", "-e", "@sky",
+                                                     "-p", "1872", "1000", "64", "64"], False),
+    "cfg5_bunny_env_4k_s1024_crop2": ("CBbunny.dae", ["-s", "1024", "-r", "3840", "2160", "-e", "@sky",
+                                                      "-p", "1888", "1096", "64", "64"], False),
+    "env_bunny_96x72_s16": ("CBbunny.dae", ["-s", "16", "-r", "96", "72", "-e", "@sky"], True),
+    "env_spheres_96x72_s16_m2": ("CBspheres_lambertian.dae", ["-s", "16", "-m", "2", "-r", "96", "72", "-e", "@sky"],
+                                 True),
+    "env_spheres_96x72_s8_hemi": ("CBspheres_lambertian.dae", ["-s", "8", "-H", "-r", "96", "72", "-e", "@sky"], True),
+    "env_spheres_96x72_s32_l2": ("CBspheres_lambertian.dae", ["-s", "32", "-l", "2", "-r", "96", "72", "-e", "@sky"],
+                                 True),
 }
 # cases whose reference PNG outputs (save_image + save_sampling_rate_image, via -f) are kept as
 # ref.png / ref_rate.png, for the rrt_render CLI tests
@@ -79,6 +92,7 @@ KEEP_PNG = {"cfg1_spheres_480x360_s8", "bunny_1080p_s64_crop", "spheres_96x72_s8
 sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
 import rrt_scenes  # noqa: E402
 GENERATED = {"@cfg4": rrt_scenes.write_cfg4_dae}
+ENVMAPS = {"@sky": rrt_scenes.write_cfg5_envmap}  # generated -e files (digest recorded in case.json)
 
 
 def run(cmd, **kw):
@@ -94,11 +108,24 @@ def dae_path(dae, workdir):
     return os.path.join(DAE, dae)
 
 
+def resolve_args(args, workdir):
+    out = []
+    for a in args:
+        if a in ENVMAPS:
+            path = os.path.join(workdir, a[1:] + ".exr")
+            ENVMAPS[a](path)
+            a = path
+        out.append(a)
+    return out
+
+
 def render(dae, args, workdir, threads, seed=0):
     prefix = os.path.join(workdir, "ref")
     cmd = [os.path.join(BIN, "ref_render"), "-t", str(threads), "-S", str(seed), "-O", prefix,
-           "-f", os.path.join(workdir, "out.png")] + args + [dae_path(dae, workdir)]
-    run(cmd, stdout=subprocess.DEVNULL)
+           "-f", os.path.join(workdir, "out.png")] + resolve_args(args, workdir) + [dae_path(dae, workdir)]
+    # cwd: EnvironmentLight::init writes probability_debug.png into the working directory (its
+    # marginal_y table, never zeroed by the reference, is zeroed by the harness: harness_exr.cpp)
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, cwd=workdir)
     return prefix
 
 
@@ -175,6 +202,10 @@ def main():
             with tempfile.TemporaryDirectory() as td:
                 info["dae_sha256"] = GENERATED[dae](os.path.join(td, "x.dae"))
             info["rrts_sha256"] = scene_sha  # the reference loader's flattened scene
+        for k, v in ENVMAPS.items():
+            if k in args:
+                with tempfile.TemporaryDirectory() as td:
+                    info["envmap_sha256"] = v(os.path.join(td, "e.exr"))
         if counters:
             info["bbox_tests"] = int(px["bbox_tests"].astype(np.int64).sum())
             info["micro_steps"] = int(px["micro_steps"].astype(np.int64).sum())

@@ -35,6 +35,23 @@ def generated_scene(tag, want_dae_sha, want_rrts_sha):
     return out
 
 
+def generated_envmap(tag, want_sha):
+    """Texels of a generated environment map ("@sky"), written as EXR by rrt_scenes and read back
+    through the product's EXR loader; the file digest must be the one the golden used."""
+    sys.path.insert(0, PKG)
+    import rrt
+    import rrt_scenes
+    d = os.path.join(tempfile.gettempdir(), "rrt_golden_gen")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, f"{tag[1:]}_{want_sha[:16]}.exr")
+    if not os.path.exists(path):
+        tmp = path + ".tmp%d" % os.getpid()
+        got = {"@sky": rrt_scenes.write_cfg5_envmap}[tag](tmp)
+        assert got == want_sha, f"{tag}: generated EXR differs from the golden's ({got})"
+        os.replace(tmp, path)
+    return rrt.load_exr(path)
+
+
 def parse_args(args):
     """Reference CLI flags (main.cpp:88-145) -> render settings."""
     cfg = dict(ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32, max_tolerance=0.05,
@@ -50,6 +67,7 @@ def parse_args(args):
         elif a == "-B": cfg["bh"] = tuple(float(v) for v in args[i + 1:i + 6]); i += 6
         elif a == "-r": i += 3
         elif a == "-p": i += 5
+        elif a == "-e": cfg["envmap"] = args[i + 1]; i += 2
         else: raise ValueError(f"unhandled flag {a}")
     return cfg
 
@@ -66,6 +84,7 @@ class Case:
         else:
             self.scene_path = os.path.join(GOLD, self.info["scene"])
         self.camera_path = os.path.join(self.dir, "camera.rrtc")
+        self._env = None
         self.frame_w, self.frame_h = self.info["frame"]["w"], self.info["frame"]["h"]
         r = self.info["region"]
         self.x0, self.y0, self.w, self.h = r["x0"], r["y0"], r["w"], r["h"]
@@ -78,12 +97,23 @@ class Case:
         return self._px
 
     @property
+    def envmap(self):
+        """[h][w][3] float32 texels of the case's -e map, or None."""
+        tag = self.cfg.get("envmap")
+        if tag is None:
+            return None
+        if self._env is None:
+            self._env = generated_envmap(tag, self.info["envmap_sha256"])
+        return self._env
+
+    @property
     def exact(self):
         """Cases whose hot path has no per-sample transcendental (the keyed draws feed only
         + - * / sqrt): the GPU must match bit for bit.  Bounces (cos/sin), the hemisphere
-        sampler (acos/sinf/cosf) and microfacet/glass BSDFs use the device libm."""
+        sampler (acos/sinf/cosf), microfacet/glass BSDFs and the environment map (acos/atan2/
+        sin/cos) use the device libm."""
         c = self.cfg
-        return c["max_ray_depth"] <= 1 and not c["direct_hemisphere"]
+        return c["max_ray_depth"] <= 1 and not c["direct_hemisphere"] and "envmap" not in c
 
 
 def all_cases():

@@ -69,6 +69,7 @@ def lib():
                                      C.POINTER(C.c_float)]
         L.ro_camera_ray.argtypes = [C.c_double, C.c_double, _f64p, _f64p, C.c_double, C.c_double, C.c_double,
                                     C.c_double, _f64p, _f64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.ro_scene_set_envmap.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         _lib = L
     return _lib
 
@@ -84,6 +85,14 @@ class Scene:
         if getattr(self, "h", None):
             lib().ro_scene_free(self.h)
             self.h = None
+
+    def set_envmap(self, texels):
+        """texels: [h][w][3] float32 (HDRImageBuffer layout)."""
+        t = np.ascontiguousarray(texels, np.float32)
+        self._env = t
+        rc = lib().ro_scene_set_envmap(self.h, t.shape[1], t.shape[0], t.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("ro_scene_set_envmap failed")
 
     def bvh(self):
         n = lib().ro_scene_num_nodes(self.h)

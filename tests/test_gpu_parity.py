@@ -25,6 +25,7 @@ def gpu():
 
 def render(gpu, c, draws=True, counters=False, flags=0):
     gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(c.envmap)
     gpu.set_camera(rrt.load_camera(c.camera_path))
     bh = c.cfg["bh"]
     gpu.set_black_hole(bh[:3], bh[3], bh[4])
@@ -61,6 +62,8 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
 @pytest.mark.parametrize("name", SMALL)
 def test_small_cases(gpu, name, variant):
     c = Case(name)
+    if variant == "wavefront" and c.envmap is not None:
+        pytest.skip("the wavefront A/B kernel has no environment-map path (rejected by the library)")
     rgb, cnt, draws, _ = render(gpu, c, flags=VARIANTS[variant])
     print(variant, end=" ")
     check(c, rgb, cnt, draws)

@@ -12,6 +12,8 @@ from golden_cases import SMALL, Case
 
 def render_case(c, rows=None, counters=True):
     s = O.Scene(c.scene_path)
+    if c.envmap is not None:
+        s.set_envmap(c.envmap)
     cam = O.load_camera(c.camera_path)
     g = c.cfg
     p = O.make_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
