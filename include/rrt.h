@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 1
+#define RRT_ABI_VERSION 2  /* 2: rrt_spacetime_desc gained spin + axis (Kerr) */
 
 enum {
   RRT_OK = 0,
@@ -105,16 +105,26 @@ typedef struct {
 /* Replaces: PathTracer::set_camera (pathtracer.cpp:119-134). */
 int rrt_set_camera(rrt_ctx* ctx, const rrt_camera_desc* cam);
 
-enum { RRT_METRIC_SCHWARZSCHILD = 0 };
+enum { RRT_METRIC_SCHWARZSCHILD = 0, RRT_METRIC_KERR = 1 };
 typedef struct {
-  uint32_t kind;              /* RRT_METRIC_SCHWARZSCHILD (r_s = 0: the reference's flat limit) */
+  uint32_t kind;              /* RRT_METRIC_SCHWARZSCHILD (r_s = 0: the reference's flat limit)
+                                 or RRT_METRIC_KERR (build-defined, no reference) */
   uint32_t reserved;
   double center[3];           /* global_black_hole.o   (blackhole.cpp:5 default (0,1,0)) */
-  double r_s;                 /* global_black_hole.r   (default 0.1) */
-  double delta_theta;         /* global_black_hole.delta_theta (default 0.1) */
+  double r_s;                 /* global_black_hole.r   (default 0.1); Kerr: 2M */
+  double delta_theta;         /* global_black_hole.delta_theta (default 0.1); Kerr: the step's
+                                 angular size seen from the hole (h = delta_theta * r / |dx/dl|) */
+  /* Kerr only (ignored for Schwarzschild): */
+  double spin;                /* dimensionless a/M in [0, 1) */
+  double axis[3];             /* spin axis (world; normalised by the library; 0 = scene up (0,1,0)) */
 } rrt_spacetime_desc;
-/* Replaces: the `-B x y z r dtheta` override of the global black hole (main.cpp:139-145). */
+/* Replaces: the `-B x y z r dtheta` override of the global black hole (main.cpp:139-145).
+ * RRT_METRIC_KERR swaps BlackHole::next_micro_ray for an RK4 null-geodesic step in Kerr-Schild
+ * coordinates; the rest of BVHAccel::intersect (segment tests, capture = no hit) is unchanged. */
 int rrt_set_spacetime(rrt_ctx* ctx, const rrt_spacetime_desc* st);
+/* The Kerr local frame for a spin axis (ez = unit(axis), ex, ey completing a right-handed
+ * basis), so a checker can restate the integrator in the same coordinates. */
+void rrt_kerr_frame(const double* axis3, double* ex3, double* ey3, double* ez3);
 
 /* ---------------------------------------------------------------- environment map */
 typedef struct {

@@ -54,6 +54,8 @@ class PathTracer {
   void set_camera(rrt_camera_state* camera);      // not owned (:119-134)
   void set_frame_size(size_t width, size_t height);  // (:136-149)
   void set_black_hole(const double center[3], double r_s, double delta_theta);  // -B (main.cpp:139-145)
+  // Kerr spin a/M in [0, 1) about `axis` (build-defined); spin < 0: Schwarzschild
+  void set_kerr(double spin, const double axis[3] = nullptr);
   void set_seed(uint64_t seed) { seed_ = seed; }  // keyed RNG seed
   void set_band_rows(size_t rows) { band_rows_ = rows; }  // rows per GPU submission (0: whole region)
 
@@ -95,6 +97,8 @@ class PathTracer {
   rrt_envmap_desc envmap_{};
   bool has_envmap_ = false;
   double hole_c_[3] = {0.0, 1.0, 0.0}, hole_rs_ = 0.1, hole_dt_ = 0.1;  // blackhole.cpp:5
+  double kerr_spin_ = -1.0, kerr_axis_[3] = {0.0, 1.0, 0.0};           // < 0: Schwarzschild
+  void apply_spacetime();
 
   size_t frame_w_ = 0, frame_h_ = 0;
   bool render_cell_ = false;

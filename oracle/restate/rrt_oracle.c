@@ -338,7 +338,11 @@ void ro_params_default(ro_params* p) {
 /* ------------------------------------------------------------------ rays & geometry */
 typedef struct { v3 o, d; double min_t, max_t; } ray_t;
 typedef struct { v3 hit_p, w_out, n; int bsdf; } isect_t;
-typedef struct { v3 c; double r, r2, dt, cos_dt, sin_dt; int steps; } hole_t;
+typedef struct {
+  v3 c; double r, r2, dt, cos_dt, sin_dt; int steps;
+  int kerr; double m, a, a2, r_hor; v3 ex, ey, ez;  /* Kerr (build-defined) */
+  double r_esc2; int kerr_max_steps;
+} hole_t;
 
 static void hole_init(hole_t* h, const double* c, double r, double dt) {
   h->c = V(c[0], c[1], c[2]); h->r = r; h->r2 = r * r; h->dt = dt;
@@ -346,6 +350,46 @@ static void hole_init(hole_t* h, const double* c, double r, double dt) {
   int j = 0;
   while (j * dt < 2 * PI_D) ++j; /* bvh.cpp:105 */
   h->steps = j;
+  h->kerr = 0;
+}
+
+/* Kerr local frame: ez = unit(axis); ex = unit(t x ez), t the world axis least aligned with ez
+ * (z, or x when |ez.z| >= 0.9); ey = ez x ex.  (Restates rrt_kerr_frame, include/rrt.h.) */
+static void kerr_frame(const double* axis, v3* ex, v3* ey, v3* ez) {
+  const double n = sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+  v3 z = V(axis[0] / n, axis[1] / n, axis[2] / n);
+  v3 t = V(0, 0, 1);
+  if (fabs(z.z) >= 0.9) t = V(1, 0, 0);
+  v3 x = V(t.y * z.z - t.z * z.y, t.z * z.x - t.x * z.z, t.x * z.y - t.y * z.x);
+  const double xn = sqrt(x.x * x.x + x.y * x.y + x.z * x.z);
+  x = V(x.x / xn, x.y / xn, x.z / xn);
+  *ez = z; *ex = x;
+  *ey = V(z.y * x.z - z.z * x.y, z.z * x.x - z.x * x.z, z.x * x.y - z.y * x.x);
+}
+
+static void hole_init_kerr(hole_t* h, const double* c, double r_s, double dt, double spin, const double* axis) {
+  hole_init(h, c, r_s, dt);
+  h->kerr = 1;
+  double ax[3] = {axis[0], axis[1], axis[2]};
+  if (ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2] == 0) { ax[0] = 0; ax[1] = 1; ax[2] = 0; }
+  kerr_frame(ax, &h->ex, &h->ey, &h->ez);
+  h->m = 0.5 * r_s;
+  h->a = spin * h->m;
+  h->a2 = h->a * h->a;
+  h->r_hor = h->m + sqrt(h->m * h->m - h->a2);
+  h->r_esc2 = INFINITY;  /* set from the scene's root box by kerr_set_escape */
+  h->kerr_max_steps = 4 * h->steps;
+}
+/* escape radius: the farthest root-box corner from the hole, at least 4M (photon orbits) */
+static void kerr_set_escape(hole_t* h, v3 lo, v3 hi) {
+  const double l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z}, c3[3] = {h->c.x, h->c.y, h->c.z};
+  double m3[3];
+  for (int k = 0; k < 3; ++k) {
+    const double dl = fabs(l3[k] - c3[k]), dh = fabs(h3[k] - c3[k]);
+    m3[k] = dl > dh ? dl : dh;
+  }
+  const double e2 = (m3[0] * m3[0] + m3[1] * m3[1]) + m3[2] * m3[2], f2 = (4.0 * h->m) * (4.0 * h->m);
+  h->r_esc2 = e2 > f2 ? e2 : f2;
 }
 
 /* BBox::intersect (bbox.cpp:10-25) */
@@ -435,6 +479,105 @@ static inline ray_t next_micro_ray(const hole_t* h, const ray_t* ray) {
   return ret;
 }
 
+/* ---- Kerr null geodesics (build-defined; restates rrt_device.h kerr_* operation for operation).
+ * Kerr-Schild Cartesian coordinates about the hole, spin along the local z:
+ *   g = eta + f l l,  f = 2 M r^3 / (r^4 + a^2 z^2),
+ *   l = (1, (r x + a y) / (r^2 + a^2), (r y - a x) / (r^2 + a^2), z / r),
+ *   r^2 = (rho^2 - a^2) / 2 + sqrt((rho^2 - a^2)^2 / 4 + a^2 z^2).
+ * H = (|p|^2 - f L^2) / 2 with p_t = -1, L = 1 + l . p:
+ *   dq/dl = p - f L l,  dp/dl = (1/2) grad(f L^2)   (gradient by forward-mode duals). */
+typedef struct { double v, x, y, z; } dn;
+static inline dn DN(double v, double x, double y, double z) { dn r = {v, x, y, z}; return r; }
+static inline dn dadd(dn a, dn b) { return DN(a.v + b.v, a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline dn dsub(dn a, dn b) { return DN(a.v - b.v, a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline dn dmul(dn a, dn b) {
+  return DN(a.v * b.v, a.x * b.v + a.v * b.x, a.y * b.v + a.v * b.y, a.z * b.v + a.v * b.z);
+}
+static inline dn dscale(double c, dn a) { return DN(c * a.v, c * a.x, c * a.y, c * a.z); }
+static inline dn ddiv(dn a, dn b) {
+  const double ib = 1.0 / b.v, q = a.v * ib;
+  return DN(q, (a.x - q * b.x) * ib, (a.y - q * b.y) * ib, (a.z - q * b.z) * ib);
+}
+static inline dn dsqrt(dn a) {
+  const double s = sqrt(a.v), k = 0.5 / s;
+  return DN(s, a.x * k, a.y * k, a.z * k);
+}
+static inline double kerr_r2(const hole_t* h, v3 q) {
+  const double w = ((q.x * q.x + q.y * q.y) + q.z * q.z) - h->a2;
+  return 0.5 * w + sqrt(0.25 * (w * w) + h->a2 * (q.z * q.z));
+}
+static inline void kerr_fl(const hole_t* h, v3 q, dn* f, dn* lx, dn* ly, dn* lz, double* r_out) {
+  const dn X = DN(q.x, 1, 0, 0), Y = DN(q.y, 0, 1, 0), Z = DN(q.z, 0, 0, 1);
+  const dn zz = dmul(Z, Z);
+  const dn w = DN(((q.x * q.x + q.y * q.y) + q.z * q.z) - h->a2, 2 * q.x, 2 * q.y, 2 * q.z);
+  const dn disc = dadd(dscale(0.25, dmul(w, w)), dscale(h->a2, zz));
+  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc));
+  const dn r = dsqrt(r2);
+  const dn den = DN(r2.v + h->a2, r2.x, r2.y, r2.z);
+  *lx = ddiv(dadd(dmul(r, X), dscale(h->a, Y)), den);
+  *ly = ddiv(dsub(dmul(r, Y), dscale(h->a, X)), den);
+  *lz = ddiv(Z, r);
+  const dn r4 = dmul(r2, r2);
+  *f = ddiv(dscale(2.0 * h->m, dmul(r, r2)), dadd(r4, dscale(h->a2, zz)));
+  *r_out = r.v;
+}
+static inline void kerr_rhs(const hole_t* h, v3 q, v3 p, v3* dq, v3* dp, double* r) {
+  dn f, lx, ly, lz;
+  kerr_fl(h, q, &f, &lx, &ly, &lz, r);
+  const dn L = dadd(dadd(dadd(DN(1.0, 0, 0, 0), dscale(p.x, lx)), dscale(p.y, ly)), dscale(p.z, lz));
+  const dn F = dmul(f, dmul(L, L));
+  const double fL = f.v * L.v;
+  *dq = V(p.x - fL * lx.v, p.y - fL * ly.v, p.z - fL * lz.v);
+  *dp = V(0.5 * F.x, 0.5 * F.y, 0.5 * F.z);
+}
+static inline v3 kerr_local(const hole_t* h, v3 v) { return V(vdot(v, h->ex), vdot(v, h->ey), vdot(v, h->ez)); }
+static inline v3 kerr_world(const hole_t* h, v3 q) {
+  return V(h->c.x + ((h->ex.x * q.x + h->ey.x * q.y) + h->ez.x * q.z),
+           h->c.y + ((h->ex.y * q.x + h->ey.y * q.y) + h->ez.y * q.z),
+           h->c.z + ((h->ex.z * q.x + h->ey.z * q.y) + h->ez.z * q.z));
+}
+/* photon at world o along world d: k = (k^t, d) made null (future root), p = g k, scaled to p_t = -1 */
+static inline void kerr_init(const hole_t* h, v3 o, v3 d, v3* q, v3* p) {
+  *q = kerr_local(h, vsub(o, h->c));
+  const v3 k = kerr_local(h, d);
+  dn f, lx, ly, lz;
+  double r;
+  kerr_fl(h, *q, &f, &lx, &ly, &lz, &r);
+  const double ld = (lx.v * k.x + ly.v * k.y) + lz.v * k.z;
+  const double A = f.v - 1.0, B = 2.0 * f.v * ld, C = 1.0 + f.v * (ld * ld);
+  double disc = B * B - 4.0 * A * C;
+  if (!(disc > 0.0)) disc = 0.0;
+  const double kt = (2.0 * C) / (sqrt(disc) - B);
+  const double pt = A * kt + f.v * ld;
+  const double s = f.v * (kt + ld);
+  *p = V(k.x + s * lx.v, k.y + s * ly.v, k.z + s * lz.v);
+  if (pt < 0.0) *p = vmul(*p, -1.0 / pt);
+}
+/* classical RK4 in the affine parameter from (q, p) with its first stage given, h = dtheta * r / |dq/dl| */
+static inline void kerr_step(const hole_t* h, v3* q, v3* p, v3 dq1, v3 dp1, double hh) {
+  v3 dq2, dp2, dq3, dp3, dq4, dp4;
+  double rr;
+  const double half = 0.5 * hh;
+  kerr_rhs(h, vadd(*q, vmul(dq1, half)), vadd(*p, vmul(dp1, half)), &dq2, &dp2, &rr);
+  kerr_rhs(h, vadd(*q, vmul(dq2, half)), vadd(*p, vmul(dp2, half)), &dq3, &dp3, &rr);
+  kerr_rhs(h, vadd(*q, vmul(dq3, hh)), vadd(*p, vmul(dp3, hh)), &dq4, &dp4, &rr);
+  const double c6 = hh / 6.0;
+  *q = vadd(*q, vmul(vadd(vadd(vadd(dq1, vmul(dq2, 2.0)), vmul(dq3, 2.0)), dq4), c6));
+  *p = vadd(*p, vmul(vadd(vadd(vadd(dp1, vmul(dp2, 2.0)), vmul(dp3, 2.0)), dp4), c6));
+}
+/* one march step: 0 = stepped, 1 = escaped (outgoing beyond r_esc); *swept += polar angle */
+static inline int kerr_advance(const hole_t* h, v3* q, v3* p, double* swept) {
+  v3 dq1, dp1;
+  double r;
+  kerr_rhs(h, *q, *p, &dq1, &dp1, &r);
+  const double rho2 = vnorm2(*q);
+  if (rho2 > h->r_esc2 && vdot(*q, dq1) > 0.0) return 1;
+  const double hh = (h->dt * r) / vnorm(dq1);
+  *swept += (hh * vnorm(vcross(*q, dq1))) / rho2;
+  kerr_step(h, q, p, dq1, dp1, hh);
+  return 0;
+}
+
 typedef struct {
   const ro_scene* s;
   hole_t hole;
@@ -461,7 +604,31 @@ static int intersect_micro(qctx* q, ray_t* r, isect_t* is, int node) {
 }
 
 /* BVHAccel::intersect (bvh.cpp:103-113): geodesic march; ray.min_t / max_t are dropped */
+static int bvh_intersect_kerr(qctx* q, v3 o, v3 d, isect_t* is) {
+  const hole_t* h = &q->hole;
+  v3 kq, kp;
+  kerr_init(h, o, d, &kq, &kp);
+  v3 a = o;
+  const double rh2 = h->r_hor * h->r_hor;
+  double swept = 0.0;
+  q->g->queries++;
+  for (int j = 0; j < h->kerr_max_steps && swept < 2.0 * PI_D; ++j) {
+    if (kerr_advance(h, &kq, &kp, &swept)) return 0; /* escaped */
+    q->g->micro_steps++;
+    if (kerr_r2(h, kq) <= rh2) return 0; /* captured: inside the outer horizon */
+    const v3 b = kerr_world(h, kq);
+    ray_t micro;
+    micro.o = a; micro.d = vsub(b, a); micro.min_t = 0.0;
+    micro.max_t = vnorm(micro.d);
+    micro.d = vnormalize(micro.d);
+    if (intersect_micro(q, &micro, is, 0)) return 1;
+    a = b;
+  }
+  return 0;
+}
+
 static int bvh_intersect(qctx* q, v3 o, v3 d, isect_t* is) {
+  if (q->hole.kerr) return bvh_intersect_kerr(q, o, d, is);
   ray_t micro; micro.o = o; micro.d = d; micro.min_t = 0.0; micro.max_t = 0.0;
   q->g->queries++;
   for (int j = 0; j < q->hole.steps; ++j) {
@@ -823,7 +990,10 @@ static spec raytrace_pixel(pctx* c, uint32_t x, uint32_t y, int32_t* count_out) 
 
 static void pctx_init(pctx* c, const ro_scene* s, const ro_camera* cam, const ro_params* p, rng_t* g) {
   c->q.s = s; c->q.g = g; c->p = p;
-  hole_init(&c->q.hole, p->bh_center, p->bh_radius, p->bh_dtheta);
+  if (p->bh_kind == 1) {
+    hole_init_kerr(&c->q.hole, p->bh_center, p->bh_radius, p->bh_dtheta, p->bh_spin, p->bh_axis);
+    kerr_set_escape(&c->q.hole, s->nodes[0].mn, s->nodes[0].mx);
+  } else hole_init(&c->q.hole, p->bh_center, p->bh_radius, p->bh_dtheta);
   c->cam_pos = V(cam->pos[0], cam->pos[1], cam->pos[2]);
   c->c2w0 = V(cam->c2w[0], cam->c2w[3], cam->c2w[6]);
   c->c2w1 = V(cam->c2w[1], cam->c2w[4], cam->c2w[7]);
@@ -890,6 +1060,33 @@ int ro_render(const ro_scene* s, const ro_camera* cam, const ro_params* p, uint3
 }
 
 /* ------------------------------------------------------------------ KAT entry points */
+int ro_kerr_chain(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame) {
+  hole_t h; hole_init_kerr(&h, bh, bh[3], bh[4], bh[5], bh + 6);
+  if (frame) {
+    frame[0] = h.ex.x; frame[1] = h.ex.y; frame[2] = h.ex.z; frame[3] = h.ey.x; frame[4] = h.ey.y;
+    frame[5] = h.ey.z; frame[6] = h.ez.x; frame[7] = h.ez.y; frame[8] = h.ez.z;
+  }
+  v3 q, p, a = V(o[0], o[1], o[2]);
+  kerr_init(&h, a, V(d[0], d[1], d[2]), &q, &p);
+  const double rh2 = h.r_hor * h.r_hor;
+  int rows = 0;
+  double swept = 0.0;
+  while (rows < max_rows) {  /* physics checks: no escape cutoff, no sweep or step budget */
+    kerr_advance(&h, &q, &p, &swept);
+    const int cap = kerr_r2(&h, q) <= rh2;
+    const v3 b = kerr_world(&h, q);
+    v3 sd = vsub(b, a);
+    const double mt = vnorm(sd);
+    sd = vnormalize(sd);
+    double* r = out + 14 * rows++;
+    r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = sd.x; r[4] = sd.y; r[5] = sd.z; r[6] = mt; r[7] = cap;
+    r[8] = q.x; r[9] = q.y; r[10] = q.z; r[11] = p.x; r[12] = p.y; r[13] = p.z;
+    if (cap) break;
+    a = b;
+  }
+  return rows;
+}
+
 int ro_micro_chain(const double* bh, const double* o, const double* d, double* out, int max_rows) {
   hole_t h; hole_init(&h, bh, bh[3], bh[4]);
   ray_t m; m.o = V(o[0], o[1], o[2]); m.d = V(d[0], d[1], d[2]); m.min_t = 0; m.max_t = 0;

@@ -49,6 +49,10 @@ typedef struct {
   uint64_t seed;
   uint32_t frame_w, frame_h;
   double bh_center[3], bh_radius, bh_dtheta;  /* global_black_hole, blackhole.cpp:5 */
+  /* Kerr (build-defined, no reference -- parity of the GPU against this restatement is the
+   * build's own; physics pinned by tests/test_kerr_oracle.py): bh_kind 1 = Kerr, spin = a/M */
+  uint32_t bh_kind, pad_;
+  double bh_spin, bh_axis[3];
 } ro_params;
 void ro_params_default(ro_params* p);
 
@@ -66,6 +70,11 @@ uint64_t ro_pixel_key(uint64_t seed, uint32_t x, uint32_t y);
 int ro_keyed_rand(uint64_t key, uint32_t n);
 /* next_micro_ray chain: writes per step (o3, d3, max_t, captured) until capture or n_steps */
 int ro_micro_chain(const double* bh /*cx,cy,cz,r,dtheta*/, const double* o, const double* d, double* out, int max_rows);
+/* Kerr geodesic chain: bh = cx,cy,cz,r_s,dtheta,spin,ax,ay,az.  Writes per step
+ * (segment start o3, unit d3, max_t, captured, q3 local position, p3 local momentum) = 14 doubles,
+ * until capture or max_rows steps (not capped at the renderer's ceil(2 pi / dtheta)); returns the
+ * number of rows.  frame (9, may be NULL): ex, ey, ez. */
+int ro_kerr_chain(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame);
 int ro_bbox_intersect(const double* mn, const double* mx, const double* o, const double* d, double min_t,
                       double max_t, double* t0, double* t1);
 int ro_tri_intersect(const double* p /*9*/, const double* n /*9*/, const double* o, const double* d,

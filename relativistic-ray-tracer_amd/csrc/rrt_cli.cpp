@@ -5,7 +5,8 @@
 //   -f F  output PNG (+ F_rate.png)    -r W H  frame size              -c F  camera settings file
 //   -a N T  adaptive batch / tolerance -H  hemisphere direct lighting  -p X Y DX DY  render a cell
 //   -b R  lens radius  -d D  focal distance  -B X Y Z R DTHETA  black hole (centre, r_s, step)
-// plus --seed S (keyed RNG seed) and --device D.  The interactive viewer is out of scope: -f is
+// plus --seed S (keyed RNG seed), --device D and --kerr A [AX AY AZ] (Kerr spin a/M about the
+// axis, default +y; build-defined).  The interactive viewer is out of scope: -f is
 // required.  Exit codes follow main.cpp (usage -> 1).
 #include <cstdio>
 #include <cstdlib>
@@ -33,6 +34,7 @@ static void usage(const char* binary) {
   std::printf("  -b  <FLOAT>      Lens radius     -d <FLOAT> Focal distance\n");
   std::printf("  -B  <X> <Y> <Z> <R> <DTHETA>  Black hole centre, Schwarzschild radius, step\n");
   std::printf("  --seed <INT>     Keyed RNG seed (default 0)   --device <INT> HIP device\n");
+  std::printf("  --kerr <A> [<AX> <AY> <AZ>]  Kerr black hole, spin a/M in [0,1) about axis (default 0 1 0)\n");
   std::printf("  -h               Print this help message\n");
 }
 
@@ -43,6 +45,7 @@ int main(int argc, char** argv) {
   bool hemi = false;
   double lens_radius = 0.25, focal_distance = 4.7;
   double hole[5] = {0.0, 1.0, 0.0, 0.1, 0.1};  // blackhole.cpp:5
+  double kerr_spin = -1.0, kerr_axis[3] = {0.0, 1.0, 0.0};    // --kerr
   size_t w = 0, h = 0, x = (size_t)-1, y = 0, dx = 0, dy = 0;
   std::string filename, cam_settings, envmap_path, scene_path;
   unsigned long long seed = 0;
@@ -80,6 +83,15 @@ int main(int argc, char** argv) {
     }
     else if (a == "--seed") { need(i, 1); seed = std::strtoull(argv[++i], nullptr, 0); }
     else if (a == "--device") { need(i, 1); device = std::atoi(argv[++i]); }
+    else if (a == "--kerr") {
+      need(i, 1);
+      kerr_spin = std::atof(argv[++i]);
+      auto num = [](const char* t) { char* e; std::strtod(t, &e); return *t && !*e; };
+      if (i + 3 < argc && num(argv[i + 1]) && num(argv[i + 2]) && num(argv[i + 3])) {
+        for (int k = 0; k < 3; ++k) kerr_axis[k] = std::atof(argv[i + 1 + k]);
+        i += 3;
+      }
+    }
     else if (!a.empty() && a[0] == '-') { usage(argv[0]); return 1; }
     else if (scene_path.empty()) scene_path = a;
     else { usage(argv[0]); return 1; }
@@ -129,6 +141,7 @@ int main(int argc, char** argv) {
                      envp, hemi, stem, lens_radius, focal_distance, device);
   pt.set_seed(seed);
   pt.set_black_hole(hole, hole[3], hole[4]);
+  if (kerr_spin >= 0) pt.set_kerr(kerr_spin, kerr_axis);
   // Application::set_up_pathtracer (application.cpp:622-628)
   pt.set_camera(&camera);
   pt.set_scene(scene);

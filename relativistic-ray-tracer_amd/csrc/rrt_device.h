@@ -422,14 +422,213 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
   o = no;
 }
 
-// BVHAccel::intersect (bvh.cpp:103-113): march the geodesic as straight micro segments; the
-// incoming ray's min_t / max_t are dropped (camera clip planes and shadow-ray distance are
-// ignored, as in the reference).  Capture by the hole returns "no hit".
+// One micro segment (o, d, max_t) against the scene -- BVHAccel::intersect_micro (bvh.cpp:115-138)
+// behind the result-identical skips -- filling *is on a hit.  Shared by the
+// Schwarzschild march below and the Kerr march (query_kerr).
 template <bool ANY, bool COUNT>
-__device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+__device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, Isect* is, Counters& cn) {
   // COUNT && kp.count_exec: count the work this path executes (grid / root skips, clean walk,
   // plane tests in the query slot) instead of the reference's
   const bool opt = !COUNT || kp.count_exec;
+  if (opt && segment_outside_root(kp, o, o + vmul(d, max_t))) return false;  // root test fails
+  if (opt && segment_clear(kp.grid, o, max_t)) return false;  // no primitive within reach
+  if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
+    const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
+                    o.y <= kp.nodes[0].mx[1] && o.z >= kp.nodes[0].mn[2] && o.z <= kp.nodes[0].mx[2];
+    if ((kp.diag & 1) || ((kp.diag & 4) && in) || ((kp.diag & 8) && !in)) return false;
+  }
+  bool clear_diag = false;
+  if (COUNT && (kp.diag & 2)) {  // diagnostic: query slot = clear segments, prim = AABB tests left
+    clear_diag = segment_clear(kp.grid, o, max_t);
+    if (clear_diag) cn.query++;
+  }
+  const uint32_t bbox_before = cn.bbox, prim_before = cn.prim;
+  int slot = -1;
+  double b1 = 0, b2 = 0, seg_t = max_t;
+  const v3 y = V(xdiv(1.0, d.x), xdiv(1.0, d.y), xdiv(1.0, d.z));
+  const bool fast = segment_fast(kp, o, d);
+  RRT_T0(tt0);
+  bool hit;
+  if (!COUNT)  // the clean tree, or the reference tree itself with no oversized list (host)
+    hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
+  else if (kp.count_exec)
+    hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
+  else
+    hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
+               : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
+  RRT_ACC(t_trav, tt0);
+  if (COUNT && (kp.diag & 2)) cn.prim = prim_before + (clear_diag ? 0u : cn.bbox - bbox_before);
+  if (!hit) return false;
+  if (!ANY) {
+    const DPrimMeta meta = kp.meta[slot];
+    is->bsdf = (int)((meta >> 8) & 0xffu);
+    is->hit_p = o + vmul(d, seg_t);
+    is->w_out = -d;
+    if (meta & 1u) {  // sphere: normal((o + d t) - c).unit()  (sphere.h:71-73)
+      const DPrimGeo gp = kp.geo[slot];
+      is->n = unit((o + vmul(d, seg_t)) - V(gp.v[0], gp.v[1], gp.v[2]));
+    } else {          // unnormalised interpolated normal (triangle.cpp:47)
+      const DPrimNrm nn = kp.nrm[slot];
+      double b0 = 1 - b1 - b2;
+      is->n = (smul(b0, V(nn.n[0], nn.n[1], nn.n[2])) + smul(b1, V(nn.n[3], nn.n[4], nn.n[5]))) +
+              smul(b2, V(nn.n[6], nn.n[7], nn.n[8]));
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ kernel variants
+// The integrator templates take an int variant V (named LEAN at the use sites):
+//   0 general, Schwarzschild;  1 LEAN: area lights only, no microfacet BSDF, importance-sampled
+//   direct light;  2 LEAN with point lights too;  V_KERR general with the Kerr march.
+// Each variant is its own kernel build, so no build carries code (and registers) it never runs.
+constexpr int V_KERR = 3;
+__host__ __device__ constexpr bool is_lean(int v) { return v == 1 || v == 2; }
+__host__ __device__ constexpr int general_of(int v) { return v == V_KERR ? V_KERR : 0; }  // non-LEAN build
+
+// ------------------------------------------------------------------ Kerr (build-defined)
+// The reference has no Kerr metric; this integrator is this build's design
+//  and oracle/restate/rrt_oracle.c restates it operation for operation.
+//
+// Kerr-Schild Cartesian coordinates about the hole (local frame ex, ey, ez = spin axis):
+//   g_mn = eta_mn + f l_m l_n,  f = 2 M r^3 / (r^4 + a^2 z^2),
+//   l_m = (1, (r x + a y) / (r^2 + a^2), (r y - a x) / (r^2 + a^2), z / r),
+//   r^2 = (rho^2 - a^2) / 2 + sqrt((rho^2 - a^2)^2 / 4 + a^2 z^2)   (Boyer-Lindquist r).
+// Photons follow H = (eta^mn p_m p_n - f (l^m p_m)^2) / 2 = 0 with p_t = -1 (E = 1):
+//   dx_i/dl = p_i - f L l_i,   dp_i/dl = (1/2) d_i (f L^2),   L = 1 + l . p.
+// The gradient d_i(f L^2) is carried by forward-mode duals (value + d/dx, d/dy, d/dz).  At
+// a = 0 the spatial coordinates are r times the unit direction, so the spatial path is the
+// Schwarzschild photon orbit u'' + u = 3 M u^2 that BlackHole::next_micro_ray steps.
+struct dn { double v, x, y, z; };
+__device__ __forceinline__ dn DN(double v, double x, double y, double z) { dn r; r.v = v; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ dn dadd(dn a, dn b) { return DN(a.v + b.v, a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ dn dsub(dn a, dn b) { return DN(a.v - b.v, a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ dn dmul(dn a, dn b) {
+  return DN(a.v * b.v, a.x * b.v + a.v * b.x, a.y * b.v + a.v * b.y, a.z * b.v + a.v * b.z);
+}
+__device__ __forceinline__ dn dscale(double c, dn a) { return DN(c * a.v, c * a.x, c * a.y, c * a.z); }
+__device__ __forceinline__ dn ddiv(dn a, dn b) {  // q = a / b, q' = (a' - q b') / b, one division
+  const double ib = xdiv(1.0, b.v), q = a.v * ib;
+  return DN(q, (a.x - q * b.x) * ib, (a.y - q * b.y) * ib, (a.z - q * b.z) * ib);
+}
+__device__ __forceinline__ dn dsqrt(dn a) {
+  const double s = xsqrt(a.v), k = xdiv(0.5, s);
+  return DN(s, a.x * k, a.y * k, a.z * k);
+}
+// r^2 (Boyer-Lindquist) at local point q, values only (capture test)
+__device__ __forceinline__ double kerr_r2(const DHole& h, v3 q) {
+  const double w = ((q.x * q.x + q.y * q.y) + q.z * q.z) - h.a2;
+  return 0.5 * w + xsqrt(0.25 * (w * w) + h.a2 * (q.z * q.z));
+}
+// f and l_i at q, with gradients; r (value) out
+__device__ __forceinline__ void kerr_fl(const DHole& h, v3 q, dn& f, dn& lx, dn& ly, dn& lz, double& r_out) {
+  const dn X = DN(q.x, 1, 0, 0), Y = DN(q.y, 0, 1, 0), Z = DN(q.z, 0, 0, 1);
+  const dn zz = dmul(Z, Z);
+  const dn w = DN(((q.x * q.x + q.y * q.y) + q.z * q.z) - h.a2, 2 * q.x, 2 * q.y, 2 * q.z);
+  const dn disc = dadd(dscale(0.25, dmul(w, w)), dscale(h.a2, zz));
+  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc));
+  const dn r = dsqrt(r2);
+  const dn den = DN(r2.v + h.a2, r2.x, r2.y, r2.z);
+  lx = ddiv(dadd(dmul(r, X), dscale(h.a, Y)), den);
+  ly = ddiv(dsub(dmul(r, Y), dscale(h.a, X)), den);
+  lz = ddiv(Z, r);
+  const dn r4 = dmul(r2, r2);
+  f = ddiv(dscale(2.0 * h.m, dmul(r, r2)), dadd(r4, dscale(h.a2, zz)));
+  r_out = r.v;
+}
+// Hamilton's equations at (q, p): dq, dp; r out
+__device__ __forceinline__ void kerr_rhs(const DHole& h, v3 q, v3 p, v3& dq, v3& dp, double& r) {
+  dn f, lx, ly, lz;
+  kerr_fl(h, q, f, lx, ly, lz, r);
+  const dn L = dadd(dadd(dadd(DN(1.0, 0, 0, 0), dscale(p.x, lx)), dscale(p.y, ly)), dscale(p.z, lz));
+  const dn F = dmul(f, dmul(L, L));
+  const double fL = f.v * L.v;
+  dq = V(p.x - fL * lx.v, p.y - fL * ly.v, p.z - fL * lz.v);
+  dp = V(0.5 * F.x, 0.5 * F.y, 0.5 * F.z);
+}
+__device__ __forceinline__ v3 kerr_local(const DHole& h, v3 v) {
+  return V(dot(v, ld3(h.ex)), dot(v, ld3(h.ey)), dot(v, ld3(h.ez)));
+}
+__device__ __forceinline__ v3 kerr_world(const DHole& h, v3 q) {
+  return V(h.c[0] + ((h.ex[0] * q.x + h.ey[0] * q.y) + h.ez[0] * q.z),
+           h.c[1] + ((h.ex[1] * q.x + h.ey[1] * q.y) + h.ez[1] * q.z),
+           h.c[2] + ((h.ex[2] * q.x + h.ey[2] * q.y) + h.ez[2] * q.z));
+}
+// Initial covector of a photon at world point o moving along world direction d: coordinate
+// velocity k = (k^t, d_local) made null (g_mn k^m k^n = 0, future root), p_m = g_mn k^n,
+// scaled to p_t = -1.
+__device__ __forceinline__ void kerr_init(const DHole& h, v3 o, v3 d, v3& q, v3& p) {
+  q = kerr_local(h, o - ld3(h.c));
+  const v3 k = kerr_local(h, d);
+  dn f, lx, ly, lz;
+  double r;
+  kerr_fl(h, q, f, lx, ly, lz, r);
+  const double ld = (lx.v * k.x + ly.v * k.y) + lz.v * k.z;
+  const double A = f.v - 1.0, B = 2.0 * f.v * ld, C = 1.0 + f.v * (ld * ld);
+  double disc = B * B - 4.0 * A * C;
+  if (!(disc > 0.0)) disc = 0.0;
+  const double kt = xdiv(2.0 * C, xsqrt(disc) - B);
+  const double pt = A * kt + f.v * ld;
+  const double s = f.v * (kt + ld);
+  p = V(k.x + s * lx.v, k.y + s * ly.v, k.z + s * lz.v);
+  if (pt < 0.0) p = vmul(p, xdiv(-1.0, pt));
+}
+// One classical RK4 step in the affine parameter from (q, p) with its first stage (dq1, dp1)
+// given, sized so the path advances delta_theta * r: h = delta_theta * r / |dq/dl|.
+__device__ __forceinline__ void kerr_step(const DHole& h, v3& q, v3& p, v3 dq1, v3 dp1, double hh) {
+  v3 dq2, dp2, dq3, dp3, dq4, dp4;
+  double rr;
+  const double half = 0.5 * hh;
+  kerr_rhs(h, q + vmul(dq1, half), p + vmul(dp1, half), dq2, dp2, rr);
+  kerr_rhs(h, q + vmul(dq2, half), p + vmul(dp2, half), dq3, dp3, rr);
+  kerr_rhs(h, q + vmul(dq3, hh), p + vmul(dp3, hh), dq4, dp4, rr);
+  const double c6 = xdiv(hh, 6.0);
+  q = q + vmul(((dq1 + vmul(dq2, 2.0)) + vmul(dq3, 2.0)) + dq4, c6);
+  p = p + vmul(((dp1 + vmul(dp2, 2.0)) + vmul(dp3, 2.0)) + dp4, c6);
+}
+// BVHAccel::intersect with the Kerr march.  Like the reference's march it
+// follows the photon for one revolution about the hole (it stops once the swept polar angle
+// reaches 2 pi; the reference takes ceil(2 pi / delta_theta) fixed-angle steps), the first
+// segment with a hit wins and capture means "no hit"; captured = the segment ends inside the
+// outer horizon.  Steps are sized by distance (accurate for radial motion too), so the sweep is
+// budgeted by angle, not by count (at most kerr_max_steps), and a photon moving outward beyond
+// every primitive (|q|^2 > r_esc2 >= (4M)^2, outside all photon orbits) has escaped: no hit.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  const DHole& h = kp.hole;
+  v3 q, p;
+  kerr_init(h, o, d, q, p);
+  v3 a = o;
+  const double rh2 = h.r_hor * h.r_hor;
+  double swept = 0.0;
+  for (int j = 0; j < h.kerr_max_steps && swept < 2.0 * PI_D; ++j) {
+    v3 dq1, dp1;
+    double r;
+    kerr_rhs(h, q, p, dq1, dp1, r);
+    const double rho2 = norm2(q);
+    if (rho2 > h.r_esc2 && dot(q, dq1) > 0.0) return false;  // outgoing beyond the scene
+    const double hh = xdiv(h.dt * r, norm(dq1));
+    swept += xdiv(hh * norm(cross(q, dq1)), rho2);           // polar angle of this step
+    kerr_step(h, q, p, dq1, dp1, hh);
+    if (COUNT) cn.micro++;
+    if (kerr_r2(h, q) <= rh2) return false;  // captured
+    const v3 b = kerr_world(h, q);
+    const v3 seg = b - a;
+    const double max_t = norm(seg);
+    const v3 sd = normalize(seg);
+    if (segment_query<ANY, COUNT>(kp, a, sd, max_t, is, cn)) return true;
+    a = b;
+  }
+  return false;
+}
+
+// BVHAccel::intersect (bvh.cpp:103-113): march the geodesic as straight micro segments; the
+// incoming ray's min_t / max_t are dropped (camera clip planes and shadow-ray distance are
+// ignored, as in the reference).  Capture by the hole returns "no hit".  KERR: the Kerr build
+// of the kernel (kernel variant V_KERR, chosen by rrt_host.cpp launch() for a Kerr spacetime).
+template <bool ANY, bool COUNT, bool KERR = false>
+__device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  if (KERR) return query_kerr<ANY, COUNT>(kp, o, d, is, cn);
   if (COUNT && !kp.count_exec && !(kp.diag & 2)) cn.query++;
   RRT_T0(tq0);
   double max_t = 0.0;
@@ -444,50 +643,7 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
       RRT_ACC(t_query, tq0);
       return false;
     }
-    if (opt && segment_outside_root(kp, o, o + vmul(d, max_t))) continue;  // root test fails
-    if (opt && segment_clear(kp.grid, o, max_t)) continue;  // no primitive within reach
-    if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
-      const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
-                      o.y <= kp.nodes[0].mx[1] && o.z >= kp.nodes[0].mn[2] && o.z <= kp.nodes[0].mx[2];
-      if ((kp.diag & 1) || ((kp.diag & 4) && in) || ((kp.diag & 8) && !in)) continue;
-    }
-    bool clear_diag = false;
-    if (COUNT && (kp.diag & 2)) {  // diagnostic: query slot = clear segments, prim = AABB tests left
-      clear_diag = segment_clear(kp.grid, o, max_t);
-      if (clear_diag) cn.query++;
-    }
-    const uint32_t bbox_before = cn.bbox, prim_before = cn.prim;
-    int slot = -1;
-    double b1 = 0, b2 = 0, seg_t = max_t;
-    const v3 y = V(xdiv(1.0, d.x), xdiv(1.0, d.y), xdiv(1.0, d.z));
-    const bool fast = segment_fast(kp, o, d);
-    RRT_T0(tt0);
-    bool hit;
-    if (!COUNT)  // the clean tree, or the reference tree itself with no oversized list (host)
-      hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
-    else if (kp.count_exec)
-      hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
-    else
-      hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
-                 : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
-    RRT_ACC(t_trav, tt0);
-    if (COUNT && (kp.diag & 2)) cn.prim = prim_before + (clear_diag ? 0u : cn.bbox - bbox_before);
-    if (hit) {
-      if (!ANY) {
-        const DPrimMeta meta = kp.meta[slot];
-        is->bsdf = (int)((meta >> 8) & 0xffu);
-        is->hit_p = o + vmul(d, seg_t);
-        is->w_out = -d;
-        if (meta & 1u) {  // sphere: normal((o + d t) - c).unit()  (sphere.h:71-73)
-          const DPrimGeo gp = kp.geo[slot];
-          is->n = unit((o + vmul(d, seg_t)) - V(gp.v[0], gp.v[1], gp.v[2]));
-        } else {          // unnormalised interpolated normal (triangle.cpp:47)
-          const DPrimNrm nn = kp.nrm[slot];
-          double b0 = 1 - b1 - b2;
-          is->n = (smul(b0, V(nn.n[0], nn.n[1], nn.n[2])) + smul(b1, V(nn.n[3], nn.n[4], nn.n[5]))) +
-                  smul(b2, V(nn.n[6], nn.n[7], nn.n[8]));
-        }
-      }
+    if (segment_query<ANY, COUNT>(kp, o, d, max_t, is, cn)) {
       RRT_ACC(t_query, tq0);
       return true;
     }
@@ -498,15 +654,15 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
 
 // query() behind a call: the caller keeps only what is live across the call, the walk gets the
 // register file to itself (rrt_sample.hip batch kernel)
-template <bool ANY>
+template <bool ANY, bool KERR>
 __device__ __noinline__ bool query_call(const KParams& kp, v3 o, v3 d, Isect* is) {
   Counters cn = {};
-  return query<ANY, false>(kp, o, d, is, cn);
+  return query<ANY, false, KERR>(kp, o, d, is, cn);
 }
-template <bool ANY, bool COUNT, bool NI>
+template <bool ANY, bool COUNT, bool NI, bool KERR = false>
 __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  if (NI && !COUNT) return query_call<ANY>(kp, o, d, is);
-  return query<ANY, COUNT>(kp, o, d, is, cn);
+  if (NI && !COUNT) return query_call<ANY, KERR>(kp, o, d, is);
+  return query<ANY, COUNT, KERR>(kp, o, d, is, cn);
 }
 
 // ------------------------------------------------------------------ BSDFs (bsdf.cpp / bsdf.h)
@@ -561,10 +717,10 @@ __device__ __forceinline__ spec mf_f(const DBsdf& b, v3 wo, v3 wi) {
   return ((mf_F(b, wi) * (float)G) * (float)D) / (float)(4 * wo.z * wi.z);
 }
 // LEAN: the scene has no microfacet BSDF (only diffuse / emission / delta BSDFs reach f)
-template <bool LEAN = false>
+template <int LEAN = 0>
 __device__ __forceinline__ spec bsdf_f(const DBsdf& b, v3 wo, v3 wi) {
   if (b.type == B_DIFFUSE) return S(b.p[0], b.p[1], b.p[2]) / (float)PI_D;
-  if (!LEAN && b.type == B_MICROFACET) return mf_f(b, wo, wi);
+  if (!is_lean(LEAN) && b.type == B_MICROFACET) return mf_f(b, wo, wi);
   return S(0, 0, 0);
 }
 __device__ __forceinline__ bool refract(v3 wo, v3& wi, float ior) {  // bsdf.cpp:146-159
@@ -683,10 +839,10 @@ __device__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float& dist, float& pd
 
 // ------------------------------------------------------------------ lights (light.cpp)
 // LEAN: every light is an area or a point light
-template <bool LEAN = false>
+template <int LEAN = 0>
 __device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
-  switch (LEAN ? (l.type == 1u ? 1u : 0u) : l.type) {
+  switch (LEAN == 1 ? 0u : LEAN == 2 ? (l.type == 1u ? 1u : 0u) : l.type) {
     case 0: {  // AreaLight::sample_L (light.cpp:80-92): float sqDist, sqrtf, float pdf
       double sx, sy;
       g.grid(sx, sy);

@@ -90,7 +90,7 @@ struct rrt_ctx {
   std::vector<uint32_t> leaf;
   uint32_t max_depth = 0;
   bool fast_div = false;  // every BVH coordinate is 0 or in [2^-800, 2^20] (qdiv, rrt_device.h)
-  bool lean = false;      // area/point lights only and no microfacet BSDF (LEAN kernel builds)
+  int lean = 0;           // LEAN kernel builds: 1 area lights only, 2 area + point lights; no microfacet BSDF
   uint32_t grid_res = 128;  // empty-space grid cells along the longest root-box axis (<= 1: none)
   std::vector<uint8_t> grid;
   DGrid hgrid{};           // host copy (k = nullptr)
@@ -627,10 +627,12 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     c->plane_eps = std::isfinite(m) ? 1e-9 * m : 0.0;
     if (c->plane_eps == 0.0) for (DPlane& pl : planes) pl = DPlane{};  // never cull
   }
-  c->lean = true;
-  for (const DLight& l : c->lights)
-    if (l.type != RRT_LIGHT_AREA && l.type != RRT_LIGHT_POINT) c->lean = false;
-  for (const DBsdf& b : c->bsdfs) if (b.type == RRT_BSDF_MICROFACET) c->lean = false;
+  c->lean = 1;
+  for (const DLight& l : c->lights) {
+    if (l.type == RRT_LIGHT_POINT && c->lean == 1) c->lean = 2;
+    if (l.type != RRT_LIGHT_AREA && l.type != RRT_LIGHT_POINT) c->lean = 0;
+  }
+  for (const DBsdf& b : c->bsdfs) if (b.type == RRT_BSDF_MICROFACET) c->lean = 0;
   c->has_scene = true;
   if (c->device < 0) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -719,16 +721,48 @@ extern "C" int rrt_set_envmap(rrt_ctx* c, const rrt_envmap_desc* env) {
 
 extern "C" int rrt_set_spacetime(rrt_ctx* c, const rrt_spacetime_desc* st) {
   if (!c || !st) return fail(c, RRT_E_INVALID, "null argument");
-  if (st->kind != RRT_METRIC_SCHWARZSCHILD) return fail(c, RRT_E_INVALID, "only the Schwarzschild metric is implemented");
+  if (st->kind != RRT_METRIC_SCHWARZSCHILD && st->kind != RRT_METRIC_KERR)
+    return fail(c, RRT_E_INVALID, "unknown metric kind");
   if (!(st->delta_theta > 0)) return fail(c, RRT_E_INVALID, "delta_theta must be > 0");
-  DHole& h = c->hole;
+  DHole h{};
   for (int i = 0; i < 3; ++i) h.c[i] = st->center[i];
   h.r = st->r_s; h.r2 = st->r_s * st->r_s; h.dt = st->delta_theta;
   h.cos_dt = std::cos(h.dt); h.sin_dt = std::sin(h.dt);  // blackhole.cpp:36-37, host libm
   int j = 0;
   while (j * h.dt < 2 * M_PI) ++j;  // bvh.cpp:105
   h.steps = j;
+  h.kind = (int32_t)st->kind;
+  if (st->kind == RRT_METRIC_KERR) {
+    // M = r_s / 2, a = spin * M, outer horizon r+ = M + sqrt(M^2 - a^2); the
+    // local frame has ez along the spin axis (default: the scene's up, +y)
+    if (!(st->r_s > 0)) return fail(c, RRT_E_INVALID, "Kerr needs r_s > 0");
+    if (!(st->spin >= 0 && st->spin < 1)) return fail(c, RRT_E_INVALID, "Kerr spin a/M must be in [0, 1)");
+    double ax[3] = {st->axis[0], st->axis[1], st->axis[2]};
+    double n = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    if (n == 0) { ax[0] = 0; ax[1] = 1; ax[2] = 0; n = 1; }
+    if (!std::isfinite(n)) return fail(c, RRT_E_INVALID, "Kerr spin axis must be finite");
+    rrt_kerr_frame(ax, h.ex, h.ey, h.ez);
+    h.m = 0.5 * st->r_s;
+    h.a = st->spin * h.m;
+    h.a2 = h.a * h.a;
+    h.r_hor = h.m + std::sqrt(h.m * h.m - h.a2);
+  }
+  c->hole = h;
   return RRT_OK;
+}
+
+extern "C" void rrt_kerr_frame(const double* axis, double* ex, double* ey, double* ez) {
+  // ez = unit(axis); ex = unit(t x ez) with t the world axis least aligned with ez; ey = ez x ex
+  const double n = std::sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+  for (int i = 0; i < 3; ++i) ez[i] = axis[i] / n;
+  double t[3] = {0, 0, 1};
+  if (std::fabs(ez[2]) >= 0.9) { t[0] = 1; t[2] = 0; }
+  double x[3] = {t[1] * ez[2] - t[2] * ez[1], t[2] * ez[0] - t[0] * ez[2], t[0] * ez[1] - t[1] * ez[0]};
+  const double xn = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  for (int i = 0; i < 3; ++i) ex[i] = x[i] / xn;
+  ey[0] = ez[1] * ex[2] - ez[2] * ex[1];
+  ey[1] = ez[2] * ex[0] - ez[0] * ex[2];
+  ey[2] = ez[0] * ex[1] - ez[1] * ex[0];
 }
 
 extern "C" int rrt_partition_tiles(uint32_t fw, uint32_t fh, uint32_t ts, uint32_t rank, uint32_t world,
@@ -797,6 +831,15 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       kp.root_lo[k] = ok ? lo[k] - c->plane_eps : -INFINITY;
       kp.root_hi[k] = ok ? hi[k] + c->plane_eps : INFINITY;
     }
+    // Kerr escape radius: the farthest root-box corner from the hole, >= 4M
+    double m3[3];
+    for (int k = 0; k < 3; ++k) {
+      const double dl = std::fabs(lo[k] - kp.hole.c[k]), dh = std::fabs(hi[k] - kp.hole.c[k]);
+      m3[k] = dl > dh ? dl : dh;
+    }
+    const double e2 = (m3[0] * m3[0] + m3[1] * m3[1]) + m3[2] * m3[2], f2 = (4.0 * kp.hole.m) * (4.0 * kp.hole.m);
+    kp.hole.r_esc2 = e2 > f2 ? e2 : f2;
+    kp.hole.kerr_max_steps = 4 * kp.hole.steps;
   }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
@@ -819,8 +862,14 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
   const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
   const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
-  const int lean = (!deep && !count && c->lean && !c->env_w && !p->direct_hemisphere) ? 1 : 0;
+  // kernel variant (rrt_device.h): the Kerr builds for a Kerr spacetime; else LEAN builds when
+  // the scene allows (no environment map, importance-sampled direct light), else general
+  const bool kerr = c->hole.kind == RRT_METRIC_KERR;
+  const int lean = kerr ? 3 /* V_KERR */
+                        : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
   if (mega && c->env_w) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel has no environment-map path");
+  if (mega && c->hole.kind != RRT_METRIC_SCHWARZSCHILD)
+    return fail(c, RRT_E_INVALID, "the wavefront A/B kernel steps the Schwarzschild metric only");
   const uint32_t wv = p->variant & 0xffu;
   const int waves = (wv >= 1 && wv <= 6) ? (int)wv : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
@@ -895,12 +944,14 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   HIPCHK(c, hipEventRecord(c->ev0, stream));
   const char* tf[2] = {"false", "true"};
-  char name[64];
+  char name[96];
   if (batch) {
     // 5 waves/SIMD measured best on cfg3 (spills are cheap; latency hiding is not)
     const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
-    const int w = lean ? bw : 2;
-    std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%s, %d>", kp.first ? (lean ? "rrt_first_kernel<true> + " : "rrt_first_kernel<false> + ") : "", tf[lean], w);
+    const int w = lean == 1 ? bw : lean == 2 ? 5 : 2;
+    char first[32] = "";
+    if (kp.first) std::snprintf(first, sizeof(first), "rrt_first_kernel<%d> + ", lean);
+    std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%d, %d>", first, lean, w);
     if (kp.first)
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
@@ -909,10 +960,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
     HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));
   } else if (pixel_loop) {
-    std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %s, ...>", tf[deep], tf[count], tf[lean]);
+    std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %d, ...>", tf[deep], tf[count], lean == 2 ? 0 : lean);
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {
-    std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %s, ...>", tf[count], tf[lean]);
+    std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %d, ...>", tf[count], lean);
     HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }
   c->last_kernel = name;

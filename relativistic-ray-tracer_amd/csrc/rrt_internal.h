@@ -68,11 +68,17 @@ struct DCamera {
   double c2w0[3], c2w1[3], c2w2[3];   // columns
   double blx, bly;                     // -tan(radians(fov)/2), host libm (part1_code.cpp:183)
 };
+enum { HOLE_SCHWARZSCHILD = 0, HOLE_KERR = 1 };  // rrt_spacetime_desc.kind
 struct DHole {
   double c[3];
   double r, r2, dt, cos_dt, sin_dt;    // cos/sin(dt) from host libm (blackhole.cpp:36-37)
   int32_t steps;                        // #{j : j * dt < 2 pi}  (bvh.cpp:105)
-  int32_t pad;
+  int32_t kind;                         // HOLE_SCHWARZSCHILD / HOLE_KERR (= RRT_METRIC_*, include/rrt.h)
+  // Kerr (rrt_device.h kerr_*): M = r_s / 2, a = spin * M, local frame (ez = spin axis)
+  double m, a, a2, r_hor;               // r_hor = M + sqrt(M^2 - a^2) (outer horizon)
+  double ex[3], ey[3], ez[3];
+  double r_esc2;                        // per launch: max(|root box corner - c|^2, (4M)^2)
+  int32_t kerr_max_steps, pad2;         // 4 * steps
 };
 
 // Empty-space grid over the root box (rrt_host.cpp build_free_grid): cell value k = Chebyshev

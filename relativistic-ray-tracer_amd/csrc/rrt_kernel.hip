@@ -13,15 +13,15 @@ namespace rrt {
 
 // ------------------------------------------------------------------ integrator (part1_code.cpp)
 // `trace` = the geodesic-marched BVH query; DEEP (bounce) builds and depth <= 1 builds share it.
-template <bool ANY, bool COUNT, bool DEEP>
+template <bool ANY, bool COUNT, bool DEEP, int LEAN>
 __device__ __forceinline__ bool trace(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  return query<ANY, COUNT>(kp, o, d, is, cn);
+  return query<ANY, COUNT, LEAN == V_KERR>(kp, o, d, is, cn);
 }
 
 // LEAN: area/point lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
 // (same values: make_coord_space is a pure function of the normal) instead of being kept live
 // across the shadow query, which keeps 12 VGPRs out of the traversal loop.
-template <bool COUNT, bool LEAN, bool DEEP>
+template <bool COUNT, int LEAN, bool DEEP>
 __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :33-57
   const DBsdf b = kp.bsdfs[is.bsdf];
   spec L = S(0, 0, 0);
@@ -37,13 +37,13 @@ __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Co
       v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
       spec contrib = ((sample * bsdf_f<LEAN>(b, to_local(f, is.w_out), w_in)) * (float)w_in.z) / pdf;
-      if (!trace<true, COUNT, DEEP>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
+      if (!trace<true, COUNT, DEEP, LEAN>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
     }
   }
   return L / (float)total;
 }
 
-template <bool COUNT, bool DEEP>
+template <bool COUNT, int LEAN, bool DEEP>
 __device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :15-31
   Frame f = coord_space(is.n);
   v3 w_out = to_local(f, is.w_out);
@@ -54,22 +54,22 @@ __device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Co
     v3 w_in = hemisphere_sample(g);
     v3 wi_world = to_world(f, w_in);
     Isect is2;
-    if (trace<false, COUNT, DEEP>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (trace<false, COUNT, DEEP, LEAN>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * bsdf_f(b, w_out, w_in)) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
 }
 
-template <bool COUNT, bool LEAN, bool DEEP>
+template <bool COUNT, int LEAN, bool DEEP>
 __device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {
-  if (LEAN) return direct_importance<COUNT, true, DEEP>(kp, g, is, cn);
-  return kp.direct_hemisphere ? direct_hemisphere<COUNT, DEEP>(kp, g, is, cn)
-                              : direct_importance<COUNT, false, DEEP>(kp, g, is, cn);
+  if (is_lean(LEAN)) return direct_importance<COUNT, LEAN, DEEP>(kp, g, is, cn);
+  return kp.direct_hemisphere ? direct_hemisphere<COUNT, general_of(LEAN), DEEP>(kp, g, is, cn)
+                              : direct_importance<COUNT, general_of(LEAN), DEEP>(kp, g, is, cn);
 }
 
 // at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
 // storing each level's terms, then folded back up in the reference's evaluation order.
-template <bool COUNT>
+template <bool COUNT, int LEAN>
 __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn) {
   spec Ld[RRT_MAX_DEPTH], smp[RRT_MAX_DEPTH], cem[RRT_MAX_DEPTH];
   float cs[RRT_MAX_DEPTH], pd[RRT_MAX_DEPTH];
@@ -81,7 +81,7 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
     v3 w_out = to_local(f, cur.w_out);
     const DBsdf b = kp.bsdfs[cur.bsdf];
     spec L_out = S(0, 0, 0);
-    if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, false, true>(kp, g, cur, cn);
+    if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, general_of(LEAN), true>(kp, g, cur, cn);
     Ld[k] = L_out;
     child[k] = false;
     dl[k] = is_delta(b);
@@ -91,7 +91,7 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
       if (pdf == 0.0f) break;
       v3 wi_world = to_world(f, w_in);
       Isect is2;
-      if (trace<false, COUNT, true>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
+      if (trace<false, COUNT, true, LEAN>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
         child[k] = true;
         smp[k] = sample; cs[k] = (float)fabs(w_in.z); pd[k] = pdf;
         cem[k] = emission(kp.bsdfs[is2.bsdf]);
@@ -115,19 +115,19 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
   return L;
 }
 
-template <bool DEEP, bool COUNT, bool LEAN>
+template <bool DEEP, bool COUNT, int LEAN>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
-  if (!trace<false, COUNT, DEEP>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
-    return (!LEAN && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
+  if (!trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
+    return (!is_lean(LEAN) && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
   if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
-  return e + at_least_one_bounce<COUNT>(kp, g, is, cn);
+  return e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
 }
 
 // PathTracer::raytrace_pixel (:125-163) with ADAPTIVE == 1, THIN_LENS == 0
-template <bool DEEP, bool COUNT, bool LEAN>
+template <bool DEEP, bool COUNT, int LEAN>
 __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
   spec ret = S(0, 0, 0);
   int n = 0;  // samples taken (the reference's i after its loop; counted explicitly: the
@@ -163,7 +163,7 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
 // DEEP: max_ray_depth >= 2 (bounce loop); COUNT: per-pixel work counters; LEAN: area lights
 // only, no microfacet BSDF, importance-sampled direct light (the BASELINE scenes); WAVES: the
 // register budget, as minimum waves per SIMD.
-template <bool DEEP, bool COUNT, bool LEAN, int WAVES>
+template <bool DEEP, bool COUNT, int LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
@@ -231,14 +231,23 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
 // ------------------------------------------------------------------ launch shims (C++ linkage)
 // Kernel selection: deep / counting variants are built once (1 wave per SIMD budget); the
 // depth <= 1 path has general and LEAN builds at 1..4 waves per SIMD (A/B knob `waves`).
+// lean = the kernel variant (rrt_device.h: 0 general, 1/2 LEAN, V_KERR).
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream) {
 #define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
-  if (deep) {
+  if (lean == rrt::V_KERR) {  // the Kerr builds (general integrator)
+    if (deep) {
+      if (count) RRT_LAUNCH(true, true, rrt::V_KERR, 1); else RRT_LAUNCH(true, false, rrt::V_KERR, 1);
+    } else if (count) {
+      RRT_LAUNCH(false, true, rrt::V_KERR, 1);
+    } else {
+      RRT_LAUNCH(false, false, rrt::V_KERR, 2);
+    }
+  } else if (deep) {
     if (count) RRT_LAUNCH(true, true, false, 1); else RRT_LAUNCH(true, false, false, 1);
   } else if (count) {
     RRT_LAUNCH(false, true, false, 1);
-  } else if (lean) {
+  } else if (lean == 1) {  // LEAN 2 (point lights) runs the general build here
     switch (waves) {
       case 1: RRT_LAUNCH(false, false, true, 1); break;
       case 3: RRT_LAUNCH(false, false, true, 3); break;

@@ -121,12 +121,18 @@ PathTracer::PathTracer(size_t ns_aa, size_t max_ray_depth, size_t ns_area_light,
     has_envmap_ = true;
     if (rrt_set_envmap(ctx_, &envmap_) != RRT_OK) err_ = rrt_last_error(ctx_);
   }
+  apply_spacetime();
+}
+
+void PathTracer::apply_spacetime() {
   rrt_spacetime_desc st;
   std::memset(&st, 0, sizeof(st));
-  st.kind = RRT_METRIC_SCHWARZSCHILD;
+  st.kind = kerr_spin_ < 0 ? RRT_METRIC_SCHWARZSCHILD : RRT_METRIC_KERR;
   for (int i = 0; i < 3; ++i) st.center[i] = hole_c_[i];
   st.r_s = hole_rs_; st.delta_theta = hole_dt_;
-  rrt_set_spacetime(ctx_, &st);
+  st.spin = kerr_spin_ < 0 ? 0.0 : kerr_spin_;
+  for (int i = 0; i < 3; ++i) st.axis[i] = kerr_axis_[i];
+  if (ctx_ && rrt_set_spacetime(ctx_, &st) != RRT_OK) err_ = rrt_last_error(ctx_);
 }
 
 PathTracer::~PathTracer() {
@@ -175,12 +181,13 @@ void PathTracer::set_frame_size(size_t width, size_t height) {
 void PathTracer::set_black_hole(const double center[3], double r_s, double delta_theta) {
   for (int i = 0; i < 3; ++i) hole_c_[i] = center[i];
   hole_rs_ = r_s; hole_dt_ = delta_theta;
-  rrt_spacetime_desc st;
-  std::memset(&st, 0, sizeof(st));
-  st.kind = RRT_METRIC_SCHWARZSCHILD;
-  for (int i = 0; i < 3; ++i) st.center[i] = center[i];
-  st.r_s = r_s; st.delta_theta = delta_theta;
-  if (ctx_ && rrt_set_spacetime(ctx_, &st) != RRT_OK) err_ = rrt_last_error(ctx_);
+  apply_spacetime();
+}
+
+void PathTracer::set_kerr(double spin, const double axis[3]) {
+  kerr_spin_ = spin;
+  if (axis) for (int i = 0; i < 3; ++i) kerr_axis_[i] = axis[i];
+  apply_spacetime();
 }
 
 rrt_render_params PathTracer::params() const {

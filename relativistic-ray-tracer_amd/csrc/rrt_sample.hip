@@ -45,7 +45,7 @@ __device__ __forceinline__ void park_hit(ShadeLds& cl, uint32_t t, const Isect& 
 
 // estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
-template <bool COUNT, bool LEAN, bool NI = false>
+template <bool COUNT, int LEAN, bool NI = false>
 __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
@@ -66,13 +66,13 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
       // only the loop state and the RNG stay in registers across the shadow query
       lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
-      if (!query_nx<true, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
+      if (!query_nx<true, COUNT, NI, LEAN == V_KERR>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
         L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
     }
   }
   return L / (float)total;
 }
-template <bool COUNT, bool LEAN>
+template <bool COUNT, int LEAN>
 __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
@@ -80,7 +80,7 @@ __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is
 }
 
 // estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
-template <bool COUNT, bool NI = false>
+template <bool COUNT, int LEAN, bool NI = false>
 __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   const int num = (int)(kp.n_lights * kp.ns_area_light);
@@ -94,16 +94,16 @@ __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl
     const v3 wi_world = to_world(f, w_in);
     const spec fw = bsdf_f(kp.bsdfs[bsdf], to_local(f, wo), w_in);
     Isect is2;
-    if (query_nx<false, COUNT, NI>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (query_nx<false, COUNT, NI, LEAN == V_KERR>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * fw) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
 }
-template <bool COUNT>
+template <bool COUNT, int LEAN>
 __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
-  return direct_hemisphere_parked<COUNT>(kp, g, cl, t, cn);
+  return direct_hemisphere_parked<COUNT, LEAN>(kp, g, cl, t, cn);
 }
 
 }  // namespace rrt
@@ -125,7 +125,7 @@ extern "C" int rrt_prof_read(unsigned long long* out) {  // out: 8 + 3 * 16384
 
 // COUNT: per-pixel work counters; LEAN: area/point lights only, no microfacet BSDF, importance-sampled
 // direct light (the BASELINE scenes); WAVES: register budget (minimum waves per SIMD).
-template <bool COUNT, bool LEAN, int WAVES>
+template <bool COUNT, int LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
@@ -212,13 +212,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
     spec s = S(0, 0, 0);
     {
       Isect is;
-      if (query<false, COUNT>(kp, ld3(cam.pos), unit(w), &is, cn)) {  // est_radiance (:103-123)
+      if (query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn)) {  // est_radiance (:103-123)
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
-        else if (LEAN) s = e + direct_importance_lds<COUNT, true>(kp, g, is, cl, t, cn);
-        else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<COUNT>(kp, g, is, cl, t, cn);
-        else s = e + direct_importance_lds<COUNT, false>(kp, g, is, cl, t, cn);
-      } else if (!LEAN && kp.env.w) {
+        else if (is_lean(LEAN)) s = e + direct_importance_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
+        else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
+        else s = e + direct_importance_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
+      } else if (!is_lean(LEAN) && kp.env.w) {
         s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
       }
     }
@@ -302,7 +302,7 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   double s1[32], s2[32];
 };
 
-template <bool LEAN, int WAVES>
+template <int LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
         const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
         Isect is;
-        hit = query_nx<false, false, RRT_BATCH_CALL>(kp, ld3(cam.pos), unit(w), &is, cn);
+        hit = query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn);
         if (hit) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
       }
       const uint32_t na = (uint32_t)__popcll(__ballot(act && hit) & lt);
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
     // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
     spec s = S(0, 0, 0);
-    if (!LEAN && act && !hit && kp.env.w) {  // miss: envLight->sample_dir of the unbent camera ray
+    if (!is_lean(LEAN) && act && !hit && kp.env.w) {  // miss: envLight->sample_dir of the unbent camera ray
       Rng g; g.key = lget(gs.key, gid); g.ctr = off;  // re-derive the ray from its jitter draws
       double jx, jy; g.grid(jx, jy);
       const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
@@ -423,9 +423,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (LEAN) s = e + direct_importance_parked<false, true, RRT_BATCH_CALL>(kp, g, cl, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, RRT_BATCH_CALL>(kp, g, cl, t, cn);
-      else s = e + direct_importance_parked<false, false, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
     }
     if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 // tile).  Its draw offset is always 0, so it needs no speculation; its hit status then seeds the
 // batch kernel's hypothesis for the pixel's other samples (all-hit and all-miss pixels -- 99.9%
 // of cfg3 -- then need a single round), and its radiance is the first term of the pixel's sums.
-template <bool LEAN>
+template <int LEAN>
 __global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
@@ -519,17 +519,17 @@ __global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __rest
     const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     Isect is;
-    const bool hit = query<false, false>(kp, ld3(cam.pos), unit(w), &is, cn);
+    const bool hit = query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn);
     spec s = S(0, 0, 0);
-    if (!hit && !LEAN && kp.env.w) s = env_dir(kp.env, unit(w));
+    if (!hit && !is_lean(LEAN) && kp.env.w) s = env_dir(kp.env, unit(w));
     if (hit) {
       park_hit(cl, t, is);
       g.ctr = kp.draws_miss;
       const spec e = emission(kp.bsdfs[is.bsdf]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (LEAN) s = e + direct_importance_parked<false, true>(kp, g, cl, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false>(kp, g, cl, t, cn);
-      else s = e + direct_importance_parked<false, false>(kp, g, cl, t, cn);
+      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN>(kp, g, cl, t, cn);
     }
     KParams::FirstSample f0;
     f0.r = s.r; f0.g = s.g; f0.b = s.b; f0.hit = hit ? 1u : 0u;
@@ -538,23 +538,29 @@ __global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __rest
 }
 
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, uint32_t grid, hipStream_t stream) {
-  if (lean) hipLaunchKernelGGL((rrt_first_kernel<true>), dim3(grid), dim3(256), 0, stream, d_kp);
-  else hipLaunchKernelGGL((rrt_first_kernel<false>), dim3(grid), dim3(256), 0, stream, d_kp);
+  if (lean == 1) hipLaunchKernelGGL((rrt_first_kernel<1>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == 2) hipLaunchKernelGGL((rrt_first_kernel<2>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == rrt::V_KERR) hipLaunchKernelGGL((rrt_first_kernel<rrt::V_KERR>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else hipLaunchKernelGGL((rrt_first_kernel<0>), dim3(grid), dim3(256), 0, stream, d_kp);
   return hipGetLastError();
 }
 
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
 #define RRT_LAUNCH_B(L, W) hipLaunchKernelGGL((rrt_batch_kernel<L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
-  if (lean) {
+  if (lean == 1) {
     switch (waves) {
-      case 2: RRT_LAUNCH_B(true, 2); break;
-      case 3: RRT_LAUNCH_B(true, 3); break;
-      case 5: RRT_LAUNCH_B(true, 5); break;
-      case 6: RRT_LAUNCH_B(true, 6); break;
-      default: RRT_LAUNCH_B(true, 5); break;
+      case 2: RRT_LAUNCH_B(1, 2); break;
+      case 3: RRT_LAUNCH_B(1, 3); break;
+      case 5: RRT_LAUNCH_B(1, 5); break;
+      case 6: RRT_LAUNCH_B(1, 6); break;
+      default: RRT_LAUNCH_B(1, 5); break;
     }
+  } else if (lean == 2) {
+    RRT_LAUNCH_B(2, 5);
+  } else if (lean == rrt::V_KERR) {
+    RRT_LAUNCH_B(rrt::V_KERR, 2);
   } else {
-    RRT_LAUNCH_B(false, 2);
+    RRT_LAUNCH_B(0, 2);
   }
 #undef RRT_LAUNCH_B
   return hipGetLastError();
@@ -563,14 +569,18 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream) {
 #define RRT_LAUNCH(C, L, W) hipLaunchKernelGGL((rrt_sample_kernel<C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
   if (count) {
-    RRT_LAUNCH(true, false, 1);
-  } else if (lean) {
+    if (lean == rrt::V_KERR) RRT_LAUNCH(true, rrt::V_KERR, 1); else RRT_LAUNCH(true, 0, 1);
+  } else if (lean == rrt::V_KERR) {
+    RRT_LAUNCH(false, rrt::V_KERR, 2);
+  } else if (lean == 1) {
     switch (waves) {
-      case 2: RRT_LAUNCH(false, true, 2); break;
-      case 4: RRT_LAUNCH(false, true, 4); break;
-      case 5: RRT_LAUNCH(false, true, 5); break;
-      default: RRT_LAUNCH(false, true, 3); break;
+      case 2: RRT_LAUNCH(false, 1, 2); break;
+      case 4: RRT_LAUNCH(false, 1, 4); break;
+      case 5: RRT_LAUNCH(false, 1, 5); break;
+      default: RRT_LAUNCH(false, 1, 3); break;
     }
+  } else if (lean == 2) {
+    RRT_LAUNCH(false, 2, 3);
   } else {
     RRT_LAUNCH(false, false, 2);
   }

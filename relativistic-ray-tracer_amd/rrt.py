@@ -64,9 +64,12 @@ class EnvmapDesc(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("texels", C.c_void_p)]
 
 
+RRT_METRIC_SCHWARZSCHILD, RRT_METRIC_KERR = 0, 1
+
+
 class SpacetimeDesc(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("center", C.c_double * 3), ("r_s", C.c_double),
-                ("delta_theta", C.c_double)]
+                ("delta_theta", C.c_double), ("spin", C.c_double), ("axis", C.c_double * 3)]
 
 
 class RenderParams(C.Structure):
@@ -92,7 +95,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
-           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save"]
+           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame"]
 
 _lib = None
 
@@ -112,6 +115,9 @@ def lib():
         L.rrt_set_scene.argtypes = [vp, vp]
         L.rrt_set_camera.argtypes = [vp, C.POINTER(CameraDesc)]
         L.rrt_set_spacetime.argtypes = [vp, C.POINTER(SpacetimeDesc)]
+        if hasattr(L, "rrt_kerr_frame"):
+            L.rrt_kerr_frame.argtypes = [vp, vp, vp, vp]
+            L.rrt_kerr_frame.restype = None
         if hasattr(L, "rrt_set_envmap"):
             L.rrt_set_envmap.argtypes = [vp, C.POINTER(EnvmapDesc)]
             L.rrt_exr_load.argtypes = [C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_uint32),
@@ -229,6 +235,14 @@ def load_camera(path):
     return cam
 
 
+def kerr_frame(axis=(0.0, 1.0, 0.0)):
+    """(ex, ey, ez) of the Kerr local frame the library uses for this spin axis."""
+    a = np.ascontiguousarray(axis, np.float64)
+    out = np.zeros((3, 3), np.float64)
+    lib().rrt_kerr_frame(a.ctypes.data, out[0].ctypes.data, out[1].ctypes.data, out[2].ctypes.data)
+    return out
+
+
 def load_exr(path):
     """Environment map texels [h][w][3] float32 (rrt_exr_load: main.cpp's load_exr)."""
     t = C.POINTER(C.c_float)()
@@ -292,11 +306,16 @@ class Renderer:
     def set_camera(self, cam):
         self._chk(lib().rrt_set_camera(self.h, C.byref(cam)))
 
-    def set_black_hole(self, center=(0.0, 1.0, 0.0), r_s=0.1, delta_theta=0.1):
+    def set_black_hole(self, center=(0.0, 1.0, 0.0), r_s=0.1, delta_theta=0.1, spin=None, axis=(0.0, 1.0, 0.0)):
+        """The global black hole (-B).  spin=None: Schwarzschild (the reference's stepper);
+        spin=a/M in [0, 1): the Kerr integrator (build-defined) about `axis`."""
         st = SpacetimeDesc()
-        st.kind = 0
+        st.kind = RRT_METRIC_SCHWARZSCHILD if spin is None else RRT_METRIC_KERR
         st.center[0], st.center[1], st.center[2] = center
         st.r_s, st.delta_theta = r_s, delta_theta
+        if spin is not None:
+            st.spin = spin
+            st.axis[0], st.axis[1], st.axis[2] = axis
         self._chk(lib().rrt_set_spacetime(self.h, C.byref(st)))
 
     def set_envmap(self, texels):

@@ -30,7 +30,8 @@ class Params(C.Structure):
                 ("samples_per_batch", C.c_uint32), ("max_tolerance", C.c_float),
                 ("direct_hemisphere", C.c_uint32), ("seed", C.c_uint64), ("frame_w", C.c_uint32),
                 ("frame_h", C.c_uint32), ("bh_center", C.c_double * 3), ("bh_radius", C.c_double),
-                ("bh_dtheta", C.c_double)]
+                ("bh_dtheta", C.c_double), ("bh_kind", C.c_uint32), ("pad_", C.c_uint32), ("bh_spin", C.c_double),
+                ("bh_axis", C.c_double * 3)]
 
 
 _lib = None
@@ -56,6 +57,7 @@ def lib():
         L.ro_pixel_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
         L.ro_keyed_rand.argtypes = [C.c_uint64, C.c_uint32]
         L.ro_micro_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int]
+        L.ro_kerr_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int, _f64p]
         L.ro_bbox_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_double, C.c_double,
                                         C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.ro_tri_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.POINTER(C.c_double), _f64p, _f64p]
@@ -113,7 +115,8 @@ def load_camera(path):
 
 
 def make_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
-                max_tolerance=0.05, direct_hemisphere=False, seed=0, bh=(0.0, 1.0, 0.0, 0.1, 0.1)):
+                max_tolerance=0.05, direct_hemisphere=False, seed=0, bh=(0.0, 1.0, 0.0, 0.1, 0.1), kerr=None):
+    """kerr: None (Schwarzschild) or (spin a/M, (ax, ay, az)) for the build-defined Kerr integrator."""
     p = Params()
     lib().ro_params_default(C.byref(p))
     p.ns_aa, p.max_ray_depth, p.ns_area_light = ns_aa, max_ray_depth, ns_area_light
@@ -121,7 +124,19 @@ def make_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, sam
     p.direct_hemisphere, p.seed, p.frame_w, p.frame_h = int(direct_hemisphere), seed, frame_w, frame_h
     p.bh_center[0], p.bh_center[1], p.bh_center[2] = bh[0], bh[1], bh[2]
     p.bh_radius, p.bh_dtheta = bh[3], bh[4]
+    if kerr is not None:
+        p.bh_kind, p.bh_spin = 1, kerr[0]
+        p.bh_axis[0], p.bh_axis[1], p.bh_axis[2] = kerr[1]
     return p
+
+
+def kerr_chain(bh, spin, axis, o, d, max_rows=64):
+    """The Kerr march of one ray: rows of (o3, d3, max_t, captured, q3, p3), and the frame (ex, ey, ez)."""
+    b = np.array(list(bh) + [spin] + list(axis), np.float64)
+    out = np.zeros((max_rows, 14), np.float64)
+    frame = np.zeros(9, np.float64)
+    n = lib().ro_kerr_chain(b, np.asarray(o, np.float64), np.asarray(d, np.float64), out, max_rows, frame)
+    return out[:n], frame.reshape(3, 3)
 
 
 def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):

@@ -22,7 +22,7 @@ def test_exports_match_header():
     L = rrt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rrt_abi_version() == 1
+    assert L.rrt_abi_version() == 2
 
 
 @pytest.fixture(scope="module")
@@ -99,6 +99,19 @@ def test_errors(host_ctx):
     st = rrt.SpacetimeDesc()
     st.delta_theta = 0.0
     assert rrt.lib().rrt_set_spacetime(host_ctx.h, C.byref(st)) == rrt.RRT_E_INVALID
+
+
+@pytest.mark.parametrize("kind,r_s,spin,ok", [(1, 0.1, 0.0, True), (1, 0.1, 0.999, True), (1, 0.1, 1.0, False),
+                                              (1, 0.1, -0.1, False), (1, 0.0, 0.5, False), (2, 0.1, 0.5, False),
+                                              (0, 0.1, 7.0, True)])
+def test_spacetime_validation(host_ctx, kind, r_s, spin, ok):
+    """Kerr needs r_s > 0 and spin a/M in [0, 1); unknown metric kinds are rejected; the spin is
+    ignored for Schwarzschild."""
+    st = rrt.SpacetimeDesc()
+    st.kind, st.r_s, st.delta_theta, st.spin = kind, r_s, 0.1, spin
+    st.center[1] = 1.0
+    rc = rrt.lib().rrt_set_spacetime(host_ctx.h, C.byref(st))
+    assert (rc == rrt.RRT_OK) == ok, rrt.lib().rrt_last_error(host_ctx.h)
 
 
 def _seg_dist(p, a, b):
