@@ -8,7 +8,8 @@ own asset (a copy under tests/golden/dae/), read by the native COLLADA ingest
 (rrt_collada_load: byte-identical to the reference loader's scene and placed camera); scene and
 camera are HBM-resident before timing.  --workload cfg4 runs BASELINE configs[3] on the
 generated 100k-triangle torus-knot scene (rrt_scenes.py; CBdragon.dae is missing upstream) at
-3840x2160, 256 spp.
+3840x2160, 256 spp; --workload cfg5 runs configs[4]: the Kerr integrator (a/M 0.9)
+with the generated HDR sky environment map, CBbunny at 3840x2160, 1024 spp.
 
 One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's 32x32
 tiles are split block-cyclically (rrt_partition_tiles); every rank renders its tiles into a
@@ -45,7 +46,21 @@ WORKLOADS = {
     "cfg4": dict(dae="@cfg4", w=3840, h=2160, spp=256, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=32,
                  desc="cfg4: torus knot (100k tris, CBdragon substitute) in CBempty, 3840x2160 256spp, "
                       "Schwarzschild, depth 1"),
+    "cfg5": dict(dae="CBbunny.dae", w=3840, h=2160, spp=1024, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=24,
+                 kerr=(0.9, (0.0, 1.0, 0.0)), env="@sky",
+                 desc="cfg5: CBbunny.dae 3840x2160 1024spp, Kerr a/M 0.9 (axis +y, r_s 0.1, dtheta 0.1) + "
+                      "1024x512 HDR sky envmap, depth 1"),
 }
+
+
+def load_workload_env(wl, workdir):
+    """The workload's environment map texels (generated sky EXR read by the native loader), or None."""
+    if not wl.get("env"):
+        return None
+    import rrt_scenes
+    path = os.path.join(workdir, "sky.exr")
+    rrt_scenes.write_cfg5_envmap(path)
+    return rrt.load_exr(path)
 
 
 def load_workload_scene(wl, workdir):
@@ -69,15 +84,17 @@ BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic byte
 BYTES_PLANE = 32  # plane-cull record (DPlane) read per plane test
 
 
-def cpu_baseline(wl, threads, row_stride, scene_path, camera_path):
+def cpu_baseline(wl, threads, row_stride, scene_path, camera_path, env=None):
     """The oracle restatement (oracle/restate, bit-exact with the reference) on the host cores,
     over every `row_stride`-th row of the same frame (a representative bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     s = O.Scene(scene_path)
+    if env is not None:
+        s.set_envmap(env)
     cam = O.load_camera(camera_path)
     c, r_s, dt = wl["bh"]
-    p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], bh=(c[0], c[1], c[2], r_s, dt))
+    p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], bh=(c[0], c[1], c[2], r_s, dt), kerr=wl.get("kerr"))
     rows = list(range(row_stride // 2, wl["h"], row_stride))
     samples = 0
     t0 = time.perf_counter()
@@ -125,7 +142,10 @@ def main():
     scene, cam_state, scene_path, camera_path = load_workload_scene(wl, workdir)
     r.set_scene(scene)
     r.set_camera(rrt.camera_desc(cam_state))
-    r.set_black_hole(*wl["bh"])
+    env = load_workload_env(wl, workdir)
+    r.set_envmap(env)
+    kerr = wl.get("kerr")
+    r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
     params = rrt.render_params(W, H, ns_aa=wl["spp"])
 
     plan = rrt_frame.FramePlan(W, H, world, TILE)
@@ -233,7 +253,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("generated torus-knot scene (rrt_scenes.py)" if wl["dae"].startswith("@") else
-                     "reference scene asset") + " via the native COLLADA ingest, keyed RNG seed 0",
+                     "reference scene asset") + " via the native COLLADA ingest" +
+                    (", generated HDR sky envmap (rrt_scenes.py)" if env is not None else "") + ", keyed RNG seed 0",
             "config": {"workload": wl["desc"], "frame": [W, H], "spp": wl["spp"], "tile": TILE,
                        "partition": f"block-cyclic {TILE}x{TILE} tiles over {world} GPU(s), RCCL gather to rank 0"},
             "samples_per_frame": int(samples),
@@ -251,7 +272,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
             out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride or wl["row_stride"], scene_path,
-                                               camera_path)
+                                               camera_path, env)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

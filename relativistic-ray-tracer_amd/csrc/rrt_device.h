@@ -395,31 +395,75 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
   return hit;
 }
 
-// BlackHole::next_micro_ray (blackhole.cpp:17-40); f4 is computed but unused there
-__device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
+// BlackHole::next_micro_ray (blackhole.cpp:17-40); f4 is computed but unused there.  Each norm
+// is computed once and its reciprocal shared: normalize(v) = v * (1 / norm(v)) (vector3D.h), and
+// u = 1 / |x| is that same reciprocal -- the same values as evaluating them separately, at half
+// the sqrt / division work.  FAST: every sqrt / division takes the bare core (sqrt_core,
+// div_core, qdiv) and `ok` collects whether all operands were in the core's exact range; the
+// caller re-runs the step with IEEE operations when one was not (rare: zero / tiny / huge
+// operands), so the result is always the IEEE one without a range branch per operation.
+template <bool FAST>
+__device__ __forceinline__ void next_micro_impl(const DHole& h, v3& o, v3& d, double& max_t, bool& ok) {
+  auto SQ = [&](double x) -> double {
+    if (!FAST) return sqrt(x);
+    ok = ok && in_core_range(x);
+    return sqrt_core(x);
+  };
+  auto DV = [&](double a, double b) -> double {
+    if (!FAST) return a / b;
+    ok = ok && in_core_range(a) && in_core_range(b);
+    return div_core(a, b);
+  };
+  auto RC = [&](double b) -> double {  // 1 / b
+    if (!FAST) return 1.0 / b;
+    ok = ok && in_core_range(b);
+    return div_core(1.0, b);
+  };
+  auto D6 = [&](double x) -> double {  // x / 6
+    if (!FAST) return x / 6.0;
+    ok = ok && in_core_range(x);
+    return qdiv(x, 6.0, 1.0 / 6.0);
+  };
   v3 no = o + vmul(d, max_t);
   v3 x_axis = no - V(h.c[0], h.c[1], h.c[2]);
-  double dist = norm(x_axis);
-  x_axis = normalize(x_axis);
-  double u = xdiv(1, dist);
+  const double dist = SQ(norm2(x_axis));
+  double u = RC(dist);
+  x_axis = V(x_axis.x * u, x_axis.y * u, x_axis.z * u);  // normalize: *= 1. / norm()
   double dx = dot(d, x_axis);
   v3 y_axis = d - smul(dx, x_axis);
-  double dy = norm(y_axis);
-  y_axis = normalize(y_axis);
-  double up = xdiv(-u * dx, dy);
+  double dy = SQ(norm2(y_axis));
+  const double idy = RC(dy);
+  y_axis = V(y_axis.x * idy, y_axis.y * idy, y_axis.z * idy);
+  double up = DV(-u * dx, dy);
   const double dt = h.dt, k = 3.0 * h.r;
   double f1 = -u + k * u * u / 2.0;
   double u2 = u + up * dt / 2.0;
   double f2 = -u2 + k * u2 * u2 / 2.0;
   double u3 = u + up * dt / 2.0 + f1 * dt * dt / 4.0;
   double f3 = -u3 + k * u3 * u3 / 2.0;
-  u += up * dt + (f1 + f2 + f3) * dt * dt / 6.0;
-  double dd = xdiv(1, u);
+  u += up * dt + D6((f1 + f2 + f3) * dt * dt);
+  double dd = RC(u);
   double next_x = dd * h.cos_dt, next_y = dd * h.sin_dt;
   v3 nd = ((V(h.c[0], h.c[1], h.c[2]) + smul(next_x, x_axis)) + smul(next_y, y_axis)) - no;
-  max_t = norm(nd);
-  d = normalize(nd);
+  max_t = SQ(norm2(nd));
+  const double inv = RC(max_t);
+  d = V(nd.x * inv, nd.y * inv, nd.z * inv);
   o = no;
+}
+__device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
+  if (RRT_LIBM_DIVSQRT) {
+    bool ok = true;
+    next_micro_impl<false>(h, o, d, max_t, ok);
+    return;
+  }
+  const v3 o0 = o, d0 = d;
+  const double m0 = max_t;
+  bool ok = true;
+  next_micro_impl<true>(h, o, d, max_t, ok);
+  if (__builtin_expect(!ok, 0)) {  // some operand outside the core's range: the IEEE step
+    o = o0; d = d0; max_t = m0;
+    next_micro_impl<false>(h, o, d, max_t, ok);
+  }
 }
 
 // One micro segment (o, d, max_t) against the scene -- BVHAccel::intersect_micro (bvh.cpp:115-138)
@@ -615,7 +659,8 @@ __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect*
     const v3 b = kerr_world(h, q);
     const v3 seg = b - a;
     const double max_t = norm(seg);
-    const v3 sd = normalize(seg);
+    const double inv = xdiv(1., max_t);
+    const v3 sd = V(seg.x * inv, seg.y * inv, seg.z * inv);  // normalize(seg), norm shared
     if (segment_query<ANY, COUNT>(kp, a, sd, max_t, is, cn)) return true;
     a = b;
   }

@@ -23,6 +23,7 @@ for step in "$@"; do
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
     bench4) run bench4 600 python3 bench.py --workload cfg4 --steps 2 --warmup 1 ;;
+    bench5) run bench5 900 python3 bench.py --workload cfg5 --steps 1 --warmup 1 ;;
     traffic) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run traffic 60 python3 tools/pmc_traffic.py ;;
