@@ -544,6 +544,23 @@ __host__ __device__ constexpr int general_of(int v) { return v == V_KERR ? V_KER
 // a = 0 the spatial coordinates are r times the unit direction, so the spatial path is the
 // Schwarzschild photon orbit u'' + u = 3 M u^2 that BlackHole::next_micro_ray steps.
 struct dn { double v, x, y, z; };
+// Arithmetic of one Kerr step (next_micro_impl's scheme): FAST takes the bare sqrt / division
+// cores and records in `ok` whether every operand lay in their exact range (a +0 numerator is
+// exact too); the caller re-runs the step IEEE (FAST = false) when one did not.
+template <bool FAST>
+struct KArith {
+  bool ok = true;
+  __device__ __forceinline__ double sq(double x) {
+    if (!FAST) return sqrt(x);
+    ok = ok && in_core_range(x);
+    return sqrt_core(x);
+  }
+  __device__ __forceinline__ double dv(double a, double b) {
+    if (!FAST) return a / b;
+    ok = ok && (in_core_range(a) || (a == 0.0 && !signbit(a))) && in_core_range(b);
+    return div_core(a, b);
+  }
+};
 __device__ __forceinline__ dn DN(double v, double x, double y, double z) { dn r; r.v = v; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ dn dadd(dn a, dn b) { return DN(a.v + b.v, a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ dn dsub(dn a, dn b) { return DN(a.v - b.v, a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -551,12 +568,14 @@ __device__ __forceinline__ dn dmul(dn a, dn b) {
   return DN(a.v * b.v, a.x * b.v + a.v * b.x, a.y * b.v + a.v * b.y, a.z * b.v + a.v * b.z);
 }
 __device__ __forceinline__ dn dscale(double c, dn a) { return DN(c * a.v, c * a.x, c * a.y, c * a.z); }
-__device__ __forceinline__ dn ddiv(dn a, dn b) {  // q = a / b, q' = (a' - q b') / b, one division
-  const double ib = xdiv(1.0, b.v), q = a.v * ib;
+template <class A>
+__device__ __forceinline__ dn ddiv(dn a, dn b, A& ar) {  // q = a / b, q' = (a' - q b') / b, one division
+  const double ib = ar.dv(1.0, b.v), q = a.v * ib;
   return DN(q, (a.x - q * b.x) * ib, (a.y - q * b.y) * ib, (a.z - q * b.z) * ib);
 }
-__device__ __forceinline__ dn dsqrt(dn a) {
-  const double s = xsqrt(a.v), k = xdiv(0.5, s);
+template <class A>
+__device__ __forceinline__ dn dsqrt(dn a, A& ar) {
+  const double s = ar.sq(a.v), k = ar.dv(0.5, s);
   return DN(s, a.x * k, a.y * k, a.z * k);
 }
 // r^2 (Boyer-Lindquist) at local point q, values only (capture test)
@@ -565,25 +584,27 @@ __device__ __forceinline__ double kerr_r2(const DHole& h, v3 q) {
   return 0.5 * w + xsqrt(0.25 * (w * w) + h.a2 * (q.z * q.z));
 }
 // f and l_i at q, with gradients; r (value) out
-__device__ __forceinline__ void kerr_fl(const DHole& h, v3 q, dn& f, dn& lx, dn& ly, dn& lz, double& r_out) {
+template <class A>
+__device__ __forceinline__ void kerr_fl(const DHole& h, v3 q, dn& f, dn& lx, dn& ly, dn& lz, double& r_out, A& ar) {
   const dn X = DN(q.x, 1, 0, 0), Y = DN(q.y, 0, 1, 0), Z = DN(q.z, 0, 0, 1);
   const dn zz = dmul(Z, Z);
   const dn w = DN(((q.x * q.x + q.y * q.y) + q.z * q.z) - h.a2, 2 * q.x, 2 * q.y, 2 * q.z);
   const dn disc = dadd(dscale(0.25, dmul(w, w)), dscale(h.a2, zz));
-  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc));
-  const dn r = dsqrt(r2);
+  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc, ar));
+  const dn r = dsqrt(r2, ar);
   const dn den = DN(r2.v + h.a2, r2.x, r2.y, r2.z);
-  lx = ddiv(dadd(dmul(r, X), dscale(h.a, Y)), den);
-  ly = ddiv(dsub(dmul(r, Y), dscale(h.a, X)), den);
-  lz = ddiv(Z, r);
+  lx = ddiv(dadd(dmul(r, X), dscale(h.a, Y)), den, ar);
+  ly = ddiv(dsub(dmul(r, Y), dscale(h.a, X)), den, ar);
+  lz = ddiv(Z, r, ar);
   const dn r4 = dmul(r2, r2);
-  f = ddiv(dscale(2.0 * h.m, dmul(r, r2)), dadd(r4, dscale(h.a2, zz)));
+  f = ddiv(dscale(2.0 * h.m, dmul(r, r2)), dadd(r4, dscale(h.a2, zz)), ar);
   r_out = r.v;
 }
 // Hamilton's equations at (q, p): dq, dp; r out
-__device__ __forceinline__ void kerr_rhs(const DHole& h, v3 q, v3 p, v3& dq, v3& dp, double& r) {
+template <class A>
+__device__ __forceinline__ void kerr_rhs(const DHole& h, v3 q, v3 p, v3& dq, v3& dp, double& r, A& ar) {
   dn f, lx, ly, lz;
-  kerr_fl(h, q, f, lx, ly, lz, r);
+  kerr_fl(h, q, f, lx, ly, lz, r, ar);
   const dn L = dadd(dadd(dadd(DN(1.0, 0, 0, 0), dscale(p.x, lx)), dscale(p.y, ly)), dscale(p.z, lz));
   const dn F = dmul(f, dmul(L, L));
   const double fL = f.v * L.v;
@@ -600,35 +621,44 @@ __device__ __forceinline__ v3 kerr_world(const DHole& h, v3 q) {
 }
 // Initial covector of a photon at world point o moving along world direction d: coordinate
 // velocity k = (k^t, d_local) made null (g_mn k^m k^n = 0, future root), p_m = g_mn k^n,
-// scaled to p_t = -1.
+// scaled to p_t = -1.  Once per query: IEEE arithmetic.
 __device__ __forceinline__ void kerr_init(const DHole& h, v3 o, v3 d, v3& q, v3& p) {
+  KArith<false> ar;
   q = kerr_local(h, o - ld3(h.c));
   const v3 k = kerr_local(h, d);
   dn f, lx, ly, lz;
   double r;
-  kerr_fl(h, q, f, lx, ly, lz, r);
+  kerr_fl(h, q, f, lx, ly, lz, r, ar);
   const double ld = (lx.v * k.x + ly.v * k.y) + lz.v * k.z;
   const double A = f.v - 1.0, B = 2.0 * f.v * ld, C = 1.0 + f.v * (ld * ld);
   double disc = B * B - 4.0 * A * C;
   if (!(disc > 0.0)) disc = 0.0;
-  const double kt = xdiv(2.0 * C, xsqrt(disc) - B);
+  const double kt = (2.0 * C) / (sqrt(disc) - B);
   const double pt = A * kt + f.v * ld;
   const double s = f.v * (kt + ld);
   p = V(k.x + s * lx.v, k.y + s * ly.v, k.z + s * lz.v);
-  if (pt < 0.0) p = vmul(p, xdiv(-1.0, pt));
+  if (pt < 0.0) p = vmul(p, -1.0 / pt);
 }
-// One classical RK4 step in the affine parameter from (q, p) with its first stage (dq1, dp1)
-// given, sized so the path advances delta_theta * r: h = delta_theta * r / |dq/dl|.
-__device__ __forceinline__ void kerr_step(const DHole& h, v3& q, v3& p, v3 dq1, v3 dp1, double hh) {
-  v3 dq2, dp2, dq3, dp3, dq4, dp4;
-  double rr;
+// One march step: the first RK4 stage at (q, p); escape test (outgoing beyond r_esc: returns
+// true); h = delta_theta * r / |dq/dl| (the path advances delta_theta * r); the polar angle
+// swept; then the classical RK4 update.
+template <class A>
+__device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, double& swept, A& ar) {
+  v3 dq1, dp1, dq2, dp2, dq3, dp3, dq4, dp4;
+  double r, rr;
+  kerr_rhs(h, q, p, dq1, dp1, r, ar);
+  const double rho2 = norm2(q);
+  if (rho2 > h.r_esc2 && dot(q, dq1) > 0.0) return true;  // outgoing beyond the scene
+  const double hh = ar.dv(h.dt * r, ar.sq(norm2(dq1)));
+  swept += ar.dv(hh * ar.sq(norm2(cross(q, dq1))), rho2);  // polar angle of this step
   const double half = 0.5 * hh;
-  kerr_rhs(h, q + vmul(dq1, half), p + vmul(dp1, half), dq2, dp2, rr);
-  kerr_rhs(h, q + vmul(dq2, half), p + vmul(dp2, half), dq3, dp3, rr);
-  kerr_rhs(h, q + vmul(dq3, hh), p + vmul(dp3, hh), dq4, dp4, rr);
-  const double c6 = xdiv(hh, 6.0);
+  kerr_rhs(h, q + vmul(dq1, half), p + vmul(dp1, half), dq2, dp2, rr, ar);
+  kerr_rhs(h, q + vmul(dq2, half), p + vmul(dp2, half), dq3, dp3, rr, ar);
+  kerr_rhs(h, q + vmul(dq3, hh), p + vmul(dp3, hh), dq4, dp4, rr, ar);
+  const double c6 = ar.dv(hh, 6.0);
   q = q + vmul(((dq1 + vmul(dq2, 2.0)) + vmul(dq3, 2.0)) + dq4, c6);
   p = p + vmul(((dp1 + vmul(dp2, 2.0)) + vmul(dp3, 2.0)) + dp4, c6);
+  return false;
 }
 // BVHAccel::intersect with the Kerr march.  Like the reference's march it
 // follows the photon for one revolution about the hole (it stops once the swept polar angle
@@ -646,14 +676,17 @@ __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect*
   const double rh2 = h.r_hor * h.r_hor;
   double swept = 0.0;
   for (int j = 0; j < h.kerr_max_steps && swept < 2.0 * PI_D; ++j) {
-    v3 dq1, dp1;
-    double r;
-    kerr_rhs(h, q, p, dq1, dp1, r);
-    const double rho2 = norm2(q);
-    if (rho2 > h.r_esc2 && dot(q, dq1) > 0.0) return false;  // outgoing beyond the scene
-    const double hh = xdiv(h.dt * r, norm(dq1));
-    swept += xdiv(hh * norm(cross(q, dq1)), rho2);           // polar angle of this step
-    kerr_step(h, q, p, dq1, dp1, hh);
+    v3 q1 = q, p1 = p;
+    double sw1 = swept;
+    KArith<!RRT_LIBM_DIVSQRT> fast;
+    bool escaped = kerr_advance(h, q1, p1, sw1, fast);
+    if (__builtin_expect(!fast.ok, 0)) {  // an operand outside the cores' range: the IEEE step
+      KArith<false> ieee;
+      q1 = q; p1 = p; sw1 = swept;
+      escaped = kerr_advance(h, q1, p1, sw1, ieee);
+    }
+    if (escaped) return false;
+    q = q1; p = p1; swept = sw1;
     if (COUNT) cn.micro++;
     if (kerr_r2(h, q) <= rh2) return false;  // captured
     const v3 b = kerr_world(h, q);
