@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="rrt_render_params.variant (A/B: waves per SIMD)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
@@ -146,7 +147,7 @@ def main():
     r.set_envmap(env)
     kerr = wl.get("kerr")
     r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
-    params = rrt.render_params(W, H, ns_aa=wl["spp"])
+    params = rrt.render_params(W, H, ns_aa=wl["spp"], variant=a.variant)
 
     plan = rrt_frame.FramePlan(W, H, world, TILE)
     tiles = plan.tiles(rank)

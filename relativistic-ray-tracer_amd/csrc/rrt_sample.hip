@@ -557,10 +557,20 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
     }
   } else if (lean == 2) {
     RRT_LAUNCH_B(2, 5);
-  } else if (lean == rrt::V_KERR) {
-    RRT_LAUNCH_B(rrt::V_KERR, 2);
+  } else if (lean == rrt::V_KERR) {  // general builds: waves/SIMD as an A/B knob
+    switch (waves) {
+      case 2: RRT_LAUNCH_B(rrt::V_KERR, 2); break;
+      case 4: RRT_LAUNCH_B(rrt::V_KERR, 4); break;
+      case 5: RRT_LAUNCH_B(rrt::V_KERR, 5); break;
+      default: RRT_LAUNCH_B(rrt::V_KERR, 3); break;
+    }
   } else {
-    RRT_LAUNCH_B(0, 2);
+    switch (waves) {
+      case 2: RRT_LAUNCH_B(0, 2); break;
+      case 4: RRT_LAUNCH_B(0, 4); break;
+      case 5: RRT_LAUNCH_B(0, 5); break;
+      default: RRT_LAUNCH_B(0, 3); break;
+    }
   }
 #undef RRT_LAUNCH_B
   return hipGetLastError();

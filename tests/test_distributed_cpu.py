@@ -15,7 +15,7 @@ import oracle_lib as O
 import rrt_frame
 from golden_cases import Case
 
-CASE = "spheres_bh_96x72_s8"
+CASE = "spheres_96x72_s8_l4"  # reference golden frame with lit pixels (2.8% non-black)
 
 
 def _free_port():
@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, out_path):
+def _rank_main(rank, world, port, out_path, kerr=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -37,7 +37,8 @@ def _rank_main(rank, world, port, out_path):
     cam = O.load_camera(c.camera_path)
     p = O.make_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
                       ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
-                      max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], bh=g["bh"])
+                      max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], bh=g["bh"],
+                      kerr=kerr)
     packed = np.zeros(plan.words, np.int32)
     prgb = packed[:plan.count_offset].view(np.float32).reshape(-1, 32, 32, 3)
     pcnt = packed[plan.count_offset:].reshape(-1, 32, 32)
@@ -63,6 +64,25 @@ def test_gather_assembles_reference_frame(tmp_path, world):
     d = np.load(out)
     assert np.array_equal(d["rgb"].view(np.uint32), c.px["rgb"].view(np.uint32))
     assert np.array_equal(d["cnt"], c.px["count"])
+    assert c.px["rgb"].max() > 0
+
+
+def test_gather_kerr_frame_is_partition_independent(tmp_path):
+    """The Kerr spacetime on 2 ranks: the assembled frame equals one
+    single-process render of the whole frame (parity against the reference: unpinned)."""
+    out = str(tmp_path / "frame.npz")
+    kerr = (0.9, (0.0, 1.0, 0.0))
+    mp.spawn(_rank_main, args=(2, _free_port(), out, kerr), nprocs=2, join=True)
+    c = Case(CASE)
+    g = c.cfg
+    p = O.make_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                      ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                      max_tolerance=g["max_tolerance"], bh=g["bh"], kerr=kerr)
+    rgb, cnt, _, _ = O.render(O.Scene(c.scene_path), O.load_camera(c.camera_path), p, 0, 0, c.frame_w, c.frame_h)
+    d = np.load(out)
+    assert np.array_equal(d["rgb"].view(np.uint32), rgb.view(np.uint32))
+    assert np.array_equal(d["cnt"], cnt)
+    assert not np.array_equal(rgb, c.px["rgb"])
 
 
 def test_plan_layout():

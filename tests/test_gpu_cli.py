@@ -33,3 +33,27 @@ def test_cli_usage_and_errors(tmp_path):
     assert subprocess.run([CLI], capture_output=True).returncode == 1
     r = subprocess.run([CLI, "-f", str(tmp_path / "x.png"), "/nonexistent.dae"], capture_output=True, text=True)
     assert r.returncode == 2 and "cannot open" in r.stderr
+
+
+def test_cli_kerr_matches_restatement(tmp_path):
+    """--kerr A: the CLI renders the Kerr spacetime; its PNG is the tonemapped
+    restatement render of the same flags (parity against the reference: unpinned, no Kerr there)."""
+    import oracle_lib as ol
+    from golden_cases import Case
+    from test_image_io import tonemap
+    case = "spheres_96x72_s8_l4"
+    c = Case(case)
+    out = str(tmp_path / "kerr.png")
+    cmd = [CLI] + c.info["args"] + ["--kerr", "0.9", "0", "1", "0", "-f", out, os.path.join(GOLD, "dae", c.info["dae"])]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    print(r.stdout[-400:], r.stderr[-400:])
+    assert r.returncode == 0
+    g = c.cfg
+    p = ol.make_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                       ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                       max_tolerance=g["max_tolerance"], bh=g["bh"], kerr=(0.9, (0.0, 1.0, 0.0)))
+    rgb, _, _, _ = ol.render(ol.Scene(c.scene_path), ol.load_camera(c.camera_path), p, 0, 0, c.frame_w, c.frame_h)
+    want = tonemap(rgb)[::-1].copy().view(np.uint8).reshape(c.frame_h, c.frame_w, 4)
+    got = read_png(out)
+    assert np.array_equal(got, want)
+    assert not np.array_equal(got, read_png(os.path.join(GOLD, case, "ref.png")))

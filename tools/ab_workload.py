@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""A/B kernel variants (rrt_render_params.variant = waves per SIMD, flags) on a bench.py workload,
+interleaved rounds in one process; prints the HIP-event kernel time per variant.
+Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402  (first: one shared HIP runtime)
+import bench  # noqa: E402
+import rrt  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="cfg5", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("variants", type=int, nargs="+")
+    a = ap.parse_args()
+    wl = bench.WORKLOADS[a.workload]
+    W, H, ts = wl["w"], wl["h"], 32
+    work = tempfile.mkdtemp(prefix="rrt_ab_")
+    r = rrt.Renderer(0)
+    scene, cam, _, _ = bench.load_workload_scene(wl, work)
+    r.set_scene(scene)
+    r.set_camera(rrt.camera_desc(cam))
+    r.set_envmap(bench.load_workload_env(wl, work))
+    kerr = wl.get("kerr")
+    r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
+    tiles = rrt.partition_tiles(W, H, ts, 0, 1)
+    n = len(tiles) * ts * ts
+    prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
+    pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    times, sums = {v: [] for v in a.variants}, {}
+    for _ in range(a.rounds):
+        for v in a.variants:
+            p = rrt.render_params(W, H, ns_aa=wl["spp"], variant=v)
+            r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+            torch.cuda.synchronize()
+            times[v].append(r.stats().last_kernel_ms)
+            sums[v] = (float(prgb.double().sum().item()), int(pcnt.long().sum().item()))
+            print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
+    same = len(set(sums.values())) == 1
+    print(json.dumps({"workload": a.workload, "identical_outputs": same,
+                      "median_ms": {v: float(np.median(t)) for v, t in times.items()}}))
+
+
+if __name__ == "__main__":
+    main()
