@@ -160,6 +160,9 @@ __device__ __forceinline__ bool in_fast_range(double v) {
   const double a = fabs(v);
   return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
 }
+#ifndef RRT_SLAB_APPROX
+#define RRT_SLAB_APPROX 1  // 0: every fast slab test takes the Markstein quotients (A/B)
+#endif
 // BBox::intersect (bbox.cpp:10-25), dividing by the segment direction; min_t is 0 for every
 // micro segment.  EXACT: IEEE division; else qdiv with the per-segment reciprocals y.
 template <bool EXACT>
@@ -170,9 +173,25 @@ __device__ __forceinline__ bool slab(const double* mn, const double* mx, v3 o, v
     ty0 = (mn[1] - o.y) / d.y; ty1 = (mx[1] - o.y) / d.y;
     tz0 = (mn[2] - o.z) / d.z; tz1 = (mx[2] - o.z) / d.z;
   } else {
-    tx0 = qdiv(mn[0] - o.x, d.x, y.x); tx1 = qdiv(mx[0] - o.x, d.x, y.x);
-    ty0 = qdiv(mn[1] - o.y, d.y, y.y); ty1 = qdiv(mx[1] - o.y, d.y, y.y);
-    tz0 = qdiv(mn[2] - o.z, d.z, y.z); tz1 = qdiv(mx[2] - o.z, d.z, y.z);
+    const double nx0 = mn[0] - o.x, nx1 = mx[0] - o.x, ny0 = mn[1] - o.y, ny1 = mx[1] - o.y,
+                 nz0 = mn[2] - o.z, nz1 = mx[2] - o.z;
+#if RRT_SLAB_APPROX
+    {  // approximate-then-verify: the products n * y are within 2^-50 (relative to the result of
+       // the min / max chains) of the exact RN(n / d) on a fast segment, so a decision that
+       // holds with a 2^-45 relative margin is the exact test's decision; the rest go exact.
+      const double ax0 = nx0 * y.x, ax1 = nx1 * y.x, ay0 = ny0 * y.y, ay1 = ny1 * y.y, az0 = nz0 * y.z,
+                   az1 = nz1 * y.z;
+      const double amin = fmax(fmax(fmin(ax0, ax1), fmin(ay0, ay1)), fmin(az0, az1)),
+                   amax = fmin(fmin(fmax(ax0, ax1), fmax(ay0, ay1)), fmax(az0, az1));
+      const double e = 0x1p-45, m1 = e * (fabs(amin) + fabs(amax)), m2 = e * (fabs(amin) + max_t),
+                   m3 = e * fabs(amax);
+      if (amin > amax + m1 || amin > max_t + m2 || amax < -m3) return false;
+      if (amin <= amax - m1 && amin <= max_t - m2 && amax >= m3) return true;
+    }
+#endif
+    tx0 = qdiv(nx0, d.x, y.x); tx1 = qdiv(nx1, d.x, y.x);
+    ty0 = qdiv(ny0, d.y, y.y); ty1 = qdiv(ny1, d.y, y.y);
+    tz0 = qdiv(nz0, d.z, y.z); tz1 = qdiv(nz1, d.z, y.z);
     // On a fast segment every quotient is finite (|d| >= 2^-800, |n - o| <= 2^21), so
     // std::min/max (NaN -> first argument) and the hardware v_min/max_f64 agree except on the
     // sign of a zero, which no comparison below can see.

@@ -950,14 +950,14 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
     // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
     const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
-    const int w = lean == 1 ? bw : lean == 2 ? 5 : gw;
+    const int w = lean == 1 ? bw : lean == 2 ? (bw >= 3 && bw <= 6 ? bw : 5) : gw;
     char first[32] = "";
     if (kp.first) std::snprintf(first, sizeof(first), "rrt_first_kernel<%d> + ", lean);
     std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%d, %d>", first, lean, w);
     if (kp.first)
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
-    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 ? bw : gw, grid, stream));
+    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
   } else if (mega) {
     std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
     HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));

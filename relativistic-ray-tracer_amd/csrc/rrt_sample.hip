@@ -556,7 +556,12 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
       default: RRT_LAUNCH_B(1, 5); break;
     }
   } else if (lean == 2) {
-    RRT_LAUNCH_B(2, 5);
+    switch (waves) {
+      case 3: RRT_LAUNCH_B(2, 3); break;
+      case 4: RRT_LAUNCH_B(2, 4); break;
+      case 6: RRT_LAUNCH_B(2, 6); break;
+      default: RRT_LAUNCH_B(2, 5); break;
+    }
   } else if (lean == rrt::V_KERR) {  // general builds: waves/SIMD as an A/B knob
     switch (waves) {
       case 2: RRT_LAUNCH_B(rrt::V_KERR, 2); break;
