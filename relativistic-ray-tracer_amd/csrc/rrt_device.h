@@ -250,6 +250,13 @@ __device__ __forceinline__ bool sphere_t(v3 c, double r2, v3 o, v3 d, double max
   if (0.0 <= t2 && t2 <= max_t) { t = t2; return true; }
   return false;
 }
+// sphere_t with tmp = o - c and |tmp|^2 already known (the hole's capture test, query())
+__device__ __forceinline__ bool sphere_t_rel(v3 tmp, double tmp2, double r2, v3 d, double max_t) {
+  double b = 2 * dot(tmp, d), cc = tmp2 - r2, disc = b * b - 4 * cc;
+  if (disc < 0) return false;
+  double t1 = (-b - sqrt(disc)) / 2, t2 = (-b + sqrt(disc)) / 2;
+  return (0.0 <= t1 && t1 <= max_t) || (0.0 <= t2 && t2 <= max_t);
+}
 // Triangle::intersect (triangle.cpp:25-55) with e1, e2 precomputed (bit-identical values)
 __device__ __forceinline__ bool tri_t(const DPrimGeo& gp, v3 o, v3 d, double max_t, double& t, double& b1o,
                                       double& b2o) {
@@ -422,7 +429,8 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
 // caller re-runs the step with IEEE operations when one was not (rare: zero / tiny / huge
 // operands), so the result is always the IEEE one without a range branch per operation.
 template <bool FAST>
-__device__ __forceinline__ void next_micro_impl(const DHole& h, v3& o, v3& d, double& max_t, bool& ok) {
+__device__ __forceinline__ void next_micro_impl(const DHole& h, v3 no, v3& o, v3& d, double& max_t, v3& rel,
+                                                double& rel2, bool& ok) {
   auto SQ = [&](double x) -> double {
     if (!FAST) return sqrt(x);
     ok = ok && in_core_range(x);
@@ -443,9 +451,10 @@ __device__ __forceinline__ void next_micro_impl(const DHole& h, v3& o, v3& d, do
     ok = ok && in_core_range(x);
     return qdiv(x, 6.0, 1.0 / 6.0);
   };
-  v3 no = o + vmul(d, max_t);
   v3 x_axis = no - V(h.c[0], h.c[1], h.c[2]);
-  const double dist = SQ(norm2(x_axis));
+  rel = x_axis;
+  rel2 = norm2(x_axis);
+  const double dist = SQ(rel2);
   double u = RC(dist);
   x_axis = V(x_axis.x * u, x_axis.y * u, x_axis.z * u);  // normalize: *= 1. / norm()
   double dx = dot(d, x_axis);
@@ -469,31 +478,39 @@ __device__ __forceinline__ void next_micro_impl(const DHole& h, v3& o, v3& d, do
   d = V(nd.x * inv, nd.y * inv, nd.z * inv);
   o = no;
 }
-__device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
+// The step from the previous segment's end point no = o + d * max_t (the caller keeps it: the
+// same value the reference computes at blackhole.cpp:18); rel = no - c and rel2 = |rel|^2 are
+// also the capture test's o - c and |o - c|^2 (sphere.cpp:12-14 on the new segment).
+__device__ __forceinline__ void next_micro_at(const DHole& h, v3 no, v3& o, v3& d, double& max_t, v3& rel,
+                                              double& rel2) {
+  bool ok = true;
   if (RRT_LIBM_DIVSQRT) {
-    bool ok = true;
-    next_micro_impl<false>(h, o, d, max_t, ok);
+    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok);
     return;
   }
-  const v3 o0 = o, d0 = d;
-  const double m0 = max_t;
-  bool ok = true;
-  next_micro_impl<true>(h, o, d, max_t, ok);
+  const v3 d0 = d;
+  next_micro_impl<true>(h, no, o, d, max_t, rel, rel2, ok);
   if (__builtin_expect(!ok, 0)) {  // some operand outside the core's range: the IEEE step
-    o = o0; d = d0; max_t = m0;
-    next_micro_impl<false>(h, o, d, max_t, ok);
+    d = d0;
+    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok);
   }
+}
+__device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
+  v3 rel;
+  double rel2;
+  next_micro_at(h, o + vmul(d, max_t), o, d, max_t, rel, rel2);
 }
 
 // One micro segment (o, d, max_t) against the scene -- BVHAccel::intersect_micro (bvh.cpp:115-138)
 // behind the result-identical skips -- filling *is on a hit.  Shared by the
 // Schwarzschild march below and the Kerr march (query_kerr).
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, Isect* is, Counters& cn) {
-  // COUNT && kp.count_exec: count the work this path executes (grid / root skips, clean walk,
-  // plane tests in the query slot) instead of the reference's
+__device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, v3 e, Isect* is,
+                                              Counters& cn) {
+  // e = o + d * max_t.  COUNT && kp.count_exec: count the work this path executes (grid / root
+  // skips, clean walk, plane tests in the query slot) instead of the reference's
   const bool opt = !COUNT || kp.count_exec;
-  if (opt && segment_outside_root(kp, o, o + vmul(d, max_t))) return false;  // root test fails
+  if (opt && segment_outside_root(kp, o, e)) return false;  // root test fails
   if (opt && segment_clear(kp.grid, o, max_t)) return false;  // no primitive within reach
   if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
     const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
@@ -713,7 +730,7 @@ __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect*
     const double max_t = norm(seg);
     const double inv = xdiv(1., max_t);
     const v3 sd = V(seg.x * inv, seg.y * inv, seg.z * inv);  // normalize(seg), norm shared
-    if (segment_query<ANY, COUNT>(kp, a, sd, max_t, is, cn)) return true;
+    if (segment_query<ANY, COUNT>(kp, a, sd, max_t, a + vmul(sd, max_t), is, cn)) return true;
     a = b;
   }
   return false;
@@ -729,18 +746,20 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   if (COUNT && !kp.count_exec && !(kp.diag & 2)) cn.query++;
   RRT_T0(tq0);
   double max_t = 0.0;
-  const v3 hc = V(kp.hole.c[0], kp.hole.c[1], kp.hole.c[2]);
+  v3 e = o + vmul(d, max_t);  // the next segment's start (micro = Ray(o, d, max_t = 0), bvh.cpp:104)
   for (int j = 0; j < kp.hole.steps; ++j) {
     RRT_T0(tm0);
-    next_micro(kp.hole, o, d, max_t);
+    v3 rel;
+    double rel2;
+    next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
     RRT_ACC(t_micro, tm0);
     if (COUNT) cn.micro++;
-    double tc;
-    if (sphere_t(hc, kp.hole.r2, o, d, max_t, tc)) {  // captured
+    if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) {  // captured
       RRT_ACC(t_query, tq0);
       return false;
     }
-    if (segment_query<ANY, COUNT>(kp, o, d, max_t, is, cn)) {
+    e = o + vmul(d, max_t);
+    if (segment_query<ANY, COUNT>(kp, o, d, max_t, e, is, cn)) {
       RRT_ACC(t_query, tq0);
       return true;
     }
