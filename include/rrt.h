@@ -243,6 +243,10 @@ int rrt_get_clean_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes, double
  * geom = {g0.x, g0.y, g0.z, 1/h, h_free}.  Returns the number of cells (0 = no grid); any
  * pointer may be NULL.  For host-side tests of its conservativeness. */
 int rrt_get_free_grid(const rrt_ctx* ctx, uint8_t* k, double* geom, int32_t* n);
+/* Per grid cell, the oversized leaves (rrt_get_clean_tree's big list, bit = index) with a
+ * primitive within reach; *reach = the segment length below which a clear bit lets the walk skip
+ * that leaf.  Returns the number of cells (0 = no masks).  Host-side tests. */
+int rrt_get_big_masks(const rrt_ctx* ctx, uint32_t* mask, double* reach);
 
 /* ---------------------------------------------------------------- file helpers (.rrts/.rrtc) */
 typedef struct rrt_scene_file rrt_scene_file;

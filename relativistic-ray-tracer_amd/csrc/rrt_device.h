@@ -221,14 +221,20 @@ __device__ __forceinline__ bool segment_fast(const KParams& kp, v3 o, v3 d) {
 // Is the micro segment [o, o + d max_t] provably clear of every BVH leaf box (DGrid)?  Then the
 // reference's traversal of it tests no primitive and returns "no hit"; skipping it is
 // result-identical.  Points outside the grid answer "not provably clear".
-__device__ __forceinline__ bool segment_clear(const DGrid& g, v3 o, double max_t) {
-  if (!g.k) return false;
+// The grid cell of point o, or -1 (no grid, or o outside it).
+__device__ __forceinline__ int grid_cell(const DGrid& g, v3 o) {
+  if (!g.k) return -1;
   const double fx = (o.x - g.g0[0]) * g.inv_h, fy = (o.y - g.g0[1]) * g.inv_h, fz = (o.z - g.g0[2]) * g.inv_h;
   if (!(fx >= 0.0 && fy >= 0.0 && fz >= 0.0 && fx < (double)g.n[0] && fy < (double)g.n[1] && fz < (double)g.n[2]))
-    return false;
+    return -1;
   const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
-  const int k = (int)g.k[(iz * g.n[1] + iy) * g.n[0] + ix];
-  return (double)(k - 2) * g.h_free > max_t;
+  return (iz * g.n[1] + iy) * g.n[0] + ix;
+}
+__device__ __forceinline__ bool cell_clear(const DGrid& g, int cell, double max_t) {
+  return cell >= 0 && (double)((int)g.k[cell] - 2) * g.h_free > max_t;
+}
+__device__ __forceinline__ bool segment_clear(const DGrid& g, v3 o, double max_t) {
+  return cell_clear(g, grid_cell(g, o), max_t);
 }
 // Does the segment [o, e] keep, along some axis, more than plane_eps (~1e6 ulps of the scene
 // scale) outside the root box?  Then the reference's first test -- the root box slab test --
@@ -377,16 +383,23 @@ __device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int c
 // is left; the oversized leaves are tested directly from a short list, merged in by their
 // left-first ordinal.  The reference's root test comes first, so rays outside the scene still
 // cost one box test.
+__device__ __forceinline__ int next_big_in(uint64_t m, int from, int nb) {  // next set bit >= from, or nb
+  const uint64_t r = from < 64 ? (m >> from) : 0ull;
+  return r ? min(from + (int)__builtin_ctzll(r), nb) : nb;
+}
+// bmask: the oversized leaves the walk must offer (bit i = kp.big[i]; the others have no
+// primitive within reach of the segment, rrt_host.cpp build_big_masks)
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
-                                               double& hb1, double& hb2, Counters& cn, bool exact) {
+                                               double& hb1, double& hb2, Counters& cn, bool exact,
+                                               uint64_t bmask = ~0ull) {
   if (COUNT) cn.bbox++;
   if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return false;
   const v3 e = o + vmul(d, max_t);  // far end point (cull only; max_t only shrinks below)
   bool hit = false;
-  int bi = 0;
   const int nb = (int)kp.n_big;
-  int next_big = nb ? kp.big[0].dfs : 0x7fffffff;
+  int bi = next_big_in(bmask, 0, nb);
+  int next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
   int node = kp.clean_root;
   // one item per iteration -- the next oversized leaf if it comes before the current node's
   // subtree in left-first order, else the node -- so both kinds share one box test and one
@@ -412,7 +425,7 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
       if (ANY) return true;
     }
     if (big) {
-      ++bi;
+      bi = next_big_in(bmask, bi + 1, nb);
       next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
     } else {
       node = (pass && count == 0) ? node + 1 : n->skip;
@@ -511,7 +524,10 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   // skips, clean walk, plane tests in the query slot) instead of the reference's
   const bool opt = !COUNT || kp.count_exec;
   if (opt && segment_outside_root(kp, o, e)) return false;  // root test fails
-  if (opt && segment_clear(kp.grid, o, max_t)) return false;  // no primitive within reach
+  const int cell = opt ? grid_cell(kp.grid, o) : -1;
+  if (cell_clear(kp.grid, cell, max_t)) return false;  // no primitive within reach
+  // oversized leaves with no primitive within reach of a short segment are not offered
+  const uint64_t bmask = (kp.big_mask && cell >= 0 && max_t < kp.big_reach) ? (uint64_t)kp.big_mask[cell] : ~0ull;
   if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
     const bool in = o.x >= kp.nodes[0].mn[0] && o.x <= kp.nodes[0].mx[0] && o.y >= kp.nodes[0].mn[1] &&
                     o.y <= kp.nodes[0].mx[1] && o.z >= kp.nodes[0].mn[2] && o.z <= kp.nodes[0].mx[2];
@@ -530,9 +546,9 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   RRT_T0(tt0);
   bool hit;
   if (!COUNT)  // the clean tree, or the reference tree itself with no oversized list (host)
-    hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
+    hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
   else if (kp.count_exec)
-    hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast);
+    hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
   else
     hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);

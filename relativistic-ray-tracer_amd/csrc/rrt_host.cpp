@@ -124,6 +124,8 @@ struct rrt_ctx {
   bool has_clean = false;
   std::vector<DNode> clean;  // host copies (rrt_get_clean_tree)
   std::vector<DBig> big;
+  std::vector<uint32_t> big_mask;   // build_big_masks (host copy; rrt_get_big_masks)
+  uint32_t* d_big_mask = nullptr;
   uint64_t device_bytes = 0;
   // per-launch workspace
   KParams* d_kp = nullptr;  // the launch's parameters (kernels take them by pointer)
@@ -163,7 +165,8 @@ static void free_scene_dev(rrt_ctx* c) {
   if (c->device < 0) return;
   hipFree(c->d_nodes); hipFree(c->d_geo); hipFree(c->d_nrm); hipFree(c->d_meta); hipFree(c->d_bsdfs);
   hipFree(c->d_lights); hipFree(c->d_grid); hipFree(c->d_clean); hipFree(c->d_big); hipFree(c->d_planes);
-  c->d_grid = nullptr; c->d_clean = nullptr; c->d_big = nullptr; c->d_planes = nullptr;
+  hipFree(c->d_big_mask);
+  c->d_grid = nullptr; c->d_clean = nullptr; c->d_big = nullptr; c->d_planes = nullptr; c->d_big_mask = nullptr;
   c->d_nodes = nullptr; c->d_geo = nullptr; c->d_nrm = nullptr; c->d_meta = nullptr; c->d_bsdfs = nullptr;
   c->d_lights = nullptr;
   c->device_bytes = 0;
@@ -287,6 +290,56 @@ static int build(rrt_ctx* c, const std::vector<uint32_t>& ids, uint32_t depth) {
 // (rounding of (p - g0) / h); any point q of a hit region lies in an occupied cell c_q, so
 // |c* - c_q|_inf >= k - 1 and |p - q| >= |p - q|_inf >= (k - 2) h.  A segment shorter than that
 // stays about a cell (~1e13 ulps) away from every hit region, so no primitive accepts it.
+// Mark the grid cells (geometry g0, h, n) holding a hit region of the leaf's primitives: for a
+// sphere its box, for a triangle the cells of its leaf box (widened by one) whose centre lies
+// within one cell of its plane (all of them for slivers).  False if a box is not finite.
+template <class F>
+static bool grid_mark_leaf(const rrt_ctx* c, const double g0[3], double h, const int32_t n[3], const Box& leaf_bb,
+                           int first, int count, F&& mark) {
+  const double inv_h = 1.0 / h;
+  auto range = [&](const V3& mn, const V3& mx, int lo[3], int hi[3]) {  // widened by one cell
+    const double a[3] = {mn.x, mn.y, mn.z}, b[3] = {mx.x, mx.y, mx.z};
+    for (int i = 0; i < 3; ++i) {
+      if (!std::isfinite(a[i]) || !std::isfinite(b[i])) return false;
+      lo[i] = std::max(0, (int)std::floor((a[i] - g0[i]) * inv_h) - 1);
+      hi[i] = std::min(n[i] - 1, (int)std::floor((b[i] - g0[i]) * inv_h) + 1);
+    }
+    return true;
+  };
+  const double reach = h * (std::sqrt(3.0) / 2 + 1.0);  // cell centre to plane: within one cell
+  int llo[3], lhi[3];
+  if (!range(leaf_bb.mn, leaf_bb.mx, llo, lhi)) return false;
+  for (int j = 0; j < count; ++j) {
+    const Prim& p = c->prims[c->leaf[first + j]];
+    int lo[3], hi[3];
+    if (p.kind == RRT_OBJ_SPHERE) {
+      const Box b = prim_box(c, p);
+      if (!range(b.mn, b.mx, lo, hi)) return false;
+      for (int z = lo[2]; z <= hi[2]; ++z)
+        for (int y = lo[1]; y <= hi[1]; ++y)
+          for (int x = lo[0]; x <= hi[0]; ++x) mark(x, y, z);
+      continue;
+    }
+    const V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
+    const V3 nn = mk(e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x);
+    const double nl = std::sqrt(nn.x * nn.x + nn.y * nn.y + nn.z * nn.z);
+    const double l1 = std::sqrt(e1.x * e1.x + e1.y * e1.y + e1.z * e1.z);
+    const double l2 = std::sqrt(e2.x * e2.x + e2.y * e2.y + e2.z * e2.z);
+    const bool sliver = !(nl >= 1e-6 * l1 * l2) || !std::isfinite(nl);
+    for (int z = llo[2]; z <= lhi[2]; ++z)
+      for (int y = llo[1]; y <= lhi[1]; ++y)
+        for (int x = llo[0]; x <= lhi[0]; ++x) {
+          if (!sliver) {
+            const double cx = g0[0] + (x + 0.5) * h, cy = g0[1] + (y + 0.5) * h, cz = g0[2] + (z + 0.5) * h;
+            const double dist = std::fabs(nn.x * (cx - p0.x) + nn.y * (cy - p0.y) + nn.z * (cz - p0.z)) / nl;
+            if (dist > reach) continue;
+          }
+          mark(x, y, z);
+        }
+  }
+  return true;
+}
+
 static void build_free_grid(rrt_ctx* c) {
   c->grid.clear();
   c->hgrid = DGrid{};
@@ -308,49 +361,9 @@ static void build_free_grid(rrt_ctx* c) {
     const size_t i = idx(x, y, z);
     if (k[i] != 0) { k[i] = 0; q.push_back((uint32_t)i); }
   };
-  // cell range of [mn, mx] widened by one cell; false if not finite
-  auto range = [&](const V3& mn, const V3& mx, int lo[3], int hi[3]) {
-    const double a[3] = {mn.x, mn.y, mn.z}, b[3] = {mx.x, mx.y, mx.z};
-    for (int i = 0; i < 3; ++i) {
-      if (!std::isfinite(a[i]) || !std::isfinite(b[i])) return false;
-      lo[i] = std::max(0, (int)std::floor((a[i] - g0[i]) * inv_h) - 1);
-      hi[i] = std::min(n[i] - 1, (int)std::floor((b[i] - g0[i]) * inv_h) + 1);
-    }
-    return true;
-  };
-  const double reach = h * (std::sqrt(3.0) / 2 + 1.0);  // cell centre to plane: within one cell
   for (const BNode& nd : c->nodes) {
     if (nd.count == 0) continue;
-    int llo[3], lhi[3];
-    if (!range(nd.bb.mn, nd.bb.mx, llo, lhi)) { c->grid.clear(); return; }
-    for (int j = 0; j < nd.count; ++j) {
-      const Prim& p = c->prims[c->leaf[nd.first + j]];
-      int lo[3], hi[3];
-      if (p.kind == RRT_OBJ_SPHERE) {
-        const Box b = prim_box(c, p);
-        if (!range(b.mn, b.mx, lo, hi)) { c->grid.clear(); return; }
-        for (int z = lo[2]; z <= hi[2]; ++z)
-          for (int y = lo[1]; y <= hi[1]; ++y)
-            for (int x = lo[0]; x <= hi[0]; ++x) mark(x, y, z);
-        continue;
-      }
-      const V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
-      const V3 nn = mk(e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x);
-      const double nl = std::sqrt(nn.x * nn.x + nn.y * nn.y + nn.z * nn.z);
-      const double l1 = std::sqrt(e1.x * e1.x + e1.y * e1.y + e1.z * e1.z);
-      const double l2 = std::sqrt(e2.x * e2.x + e2.y * e2.y + e2.z * e2.z);
-      const bool sliver = !(nl >= 1e-6 * l1 * l2) || !std::isfinite(nl);
-      for (int z = llo[2]; z <= lhi[2]; ++z)
-        for (int y = llo[1]; y <= lhi[1]; ++y)
-          for (int x = llo[0]; x <= lhi[0]; ++x) {
-            if (!sliver) {
-              const double cx = g0[0] + (x + 0.5) * h, cy = g0[1] + (y + 0.5) * h, cz = g0[2] + (z + 0.5) * h;
-              const double dist = std::fabs(nn.x * (cx - p0.x) + nn.y * (cy - p0.y) + nn.z * (cz - p0.z)) / nl;
-              if (dist > reach) continue;
-            }
-            mark(x, y, z);
-          }
-    }
+    if (!grid_mark_leaf(c, g0, h, n, nd.bb, nd.first, nd.count, mark)) { c->grid.clear(); return; }
   }
   for (size_t head = 0; head < q.size(); ++head) {  // BFS: Chebyshev distance transform
     const uint32_t i = q[head];
@@ -371,6 +384,58 @@ static void build_free_grid(rrt_ctx* c) {
   for (int i = 0; i < 3; ++i) { g.g0[i] = g0[i]; g.n[i] = n[i]; }
   g.inv_h = inv_h;
   g.h_free = h * (1.0 - 0x1p-20);
+}
+
+// Per-cell masks of the oversized leaves (traverse_clean): bit b of cell c is set when leaf b
+// has a primitive hit region within Chebyshev distance RRT_BIG_REACH cells of c (the free
+// grid's marking, dilated).  A clear bit means every point of c lies at least
+// (RRT_BIG_REACH - 1) * h_free from every primitive of leaf b (the free grid's argument with
+// k = RRT_BIG_REACH + 1), so a segment starting in c and shorter than that cannot be accepted by
+// any of them and the walk may skip the leaf without changing its answer.  Up to 32 leaves.
+static void build_big_masks(rrt_ctx* c) {
+  c->big_mask.clear();
+  if (c->grid.empty() || c->big.empty() || c->big.size() > 32) return;
+  const DGrid& g = c->hgrid;
+  const int32_t n[3] = {g.n[0], g.n[1], g.n[2]};
+  const size_t total = (size_t)n[0] * n[1] * n[2];
+  const double h = 1.0 / g.inv_h;
+  std::vector<uint32_t> mask(total, 0u);
+  std::vector<uint8_t> a(total), b(total);
+  auto idx = [&](int x, int y, int z) { return ((size_t)z * n[1] + y) * n[0] + x; };
+  const int R = RRT_BIG_REACH;
+  for (size_t bi = 0; bi < c->big.size(); ++bi) {
+    const DBig& L = c->big[bi];
+    std::fill(a.begin(), a.end(), 0);
+    Box bb;
+    bb.mn = mk(L.mn[0], L.mn[1], L.mn[2]);
+    bb.mx = mk(L.mx[0], L.mx[1], L.mx[2]);
+    if (!grid_mark_leaf(c, g.g0, h, n, bb, L.first, L.count, [&](int x, int y, int z) { a[idx(x, y, z)] = 1; })) {
+      c->big_mask.clear();
+      return;
+    }
+    // Chebyshev dilation by R: separable running max along x, y, z
+    for (int axis = 0; axis < 3; ++axis) {
+      const int len = n[axis];
+      const size_t stride = axis == 0 ? 1 : axis == 1 ? (size_t)n[0] : (size_t)n[0] * n[1];
+      const int o1 = axis == 0 ? 1 : 0, o2 = axis == 2 ? 1 : 2;  // the two other axes
+      for (int u = 0; u < n[o1]; ++u)
+        for (int v = 0; v < n[o2]; ++v) {
+          int co[3] = {0, 0, 0};
+          co[o1] = u; co[o2] = v;
+          const size_t base = idx(co[0], co[1], co[2]);
+          int cnt = 0;  // marked cells in the window [i - R, i + R]
+          for (int i = 0; i < std::min(R, len); ++i) cnt += a[base + i * stride];
+          for (int i = 0; i < len; ++i) {
+            if (i + R < len) cnt += a[base + (size_t)(i + R) * stride];
+            if (i - R - 1 >= 0) cnt -= a[base + (size_t)(i - R - 1) * stride];
+            b[base + i * stride] = cnt > 0;
+          }
+        }
+      a.swap(b);
+    }
+    for (size_t i = 0; i < total; ++i) if (a[i]) mask[i] |= 1u << bi;
+  }
+  c->big_mask.swap(mask);
 }
 
 // Clean tree for traverse_clean (rrt_device.h): the reference tree without its oversized leaves,
@@ -620,6 +685,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   }
   build_free_grid(c);
   build_clean_tree(c, c->clean, c->big);
+  build_big_masks(c);
   {  // plane-cull margin: 1e-9 of the scene's coordinate scale (rounding is ~1e-16 of it)
     const Box& rb = c->nodes[0].bb;
     double m = 1.0;
@@ -649,6 +715,9 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if (c->has_clean) {
     if ((rc = upload(c, (void**)&c->d_clean, c->clean.data(), c->clean.size() * sizeof(DNode)))) return rc;
     if ((rc = upload(c, (void**)&c->d_big, c->big.data(), c->big.size() * sizeof(DBig)))) return rc;
+    if (!c->big_mask.empty() &&
+        (rc = upload(c, (void**)&c->d_big_mask, c->big_mask.data(), c->big_mask.size() * sizeof(uint32_t))))
+      return rc;
   }
   return RRT_OK;
 }
@@ -822,6 +891,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const bool use_clean = c->has_clean && !(p->flags & RRT_RENDER_NO_CLEAN);
   kp.clean_nodes = use_clean ? c->d_clean : c->d_nodes;
   kp.big = c->d_big; kp.clean_root = 0; kp.n_big = use_clean ? c->n_big : 0u;
+  kp.big_mask = (use_clean && !(p->flags & RRT_RENDER_NO_SKIP)) ? c->d_big_mask : nullptr;
+  kp.big_reach = (RRT_BIG_REACH - 1) * c->hgrid.h_free;
   kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
   {
     const Box& rb = c->nodes[0].bb;
@@ -1105,6 +1176,13 @@ extern "C" int rrt_get_free_grid(const rrt_ctx* c, uint8_t* k, double* geom, int
   }
   if (n) for (int i = 0; i < 3; ++i) n[i] = c->hgrid.n[i];
   return (int)std::min<size_t>(c->grid.size(), 0x7fffffff);
+}
+
+extern "C" int rrt_get_big_masks(const rrt_ctx* c, uint32_t* mask, double* reach) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  if (mask && !c->big_mask.empty()) std::memcpy(mask, c->big_mask.data(), c->big_mask.size() * sizeof(uint32_t));
+  if (reach) *reach = (RRT_BIG_REACH - 1) * c->hgrid.h_free;
+  return (int)std::min<size_t>(c->big_mask.size(), 0x7fffffff);
 }
 
 extern "C" int rrt_get_clean_tree(const rrt_ctx* c, double* boxes, int32_t* nodes, double* big_boxes,

@@ -6,6 +6,7 @@
 #define RRT_MAX_LIGHTS 16
 #define RRT_MAX_BSDFS 64
 #define RRT_MAX_DEPTH 16
+#define RRT_BIG_REACH 10   // oversized-leaf cell masks: dilation radius in grid cells (rrt_host.cpp)
 
 // BVH node, 64 B, left-first pre-order (the reference's recursion order, bvh.cpp:115-138).
 // Left child of an inner node is always index + 1; `skip` is the pre-order successor of the
@@ -112,6 +113,8 @@ struct KParams {
   double root_lo[3], root_hi[3];  // root box widened by plane_eps (segment_outside_root)
   double plane_eps;           // plane-cull margin (scene-scaled, ~1e6 x rounding error)
   const DBig* big;            // oversized leaves by left-first ordinal
+  const uint32_t* big_mask;   // per grid cell: oversized leaves with a primitive in reach, or null
+  double big_reach;           // segments shorter than this may use big_mask ((RRT_BIG_REACH - 1) h_free)
   int32_t clean_root;         // 0, or -1 if every leaf is oversized
   uint32_t n_big;
   DCamera cam;

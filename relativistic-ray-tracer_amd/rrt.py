@@ -95,7 +95,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
-           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame"]
+           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks"]
 
 _lib = None
 
@@ -133,7 +133,7 @@ def lib():
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
-        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5)):
+        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_big_masks", 3)):
             if hasattr(L, name):  # absent from older builds loaded through RRT_LIB
                 getattr(L, name).argtypes = [vp] * n_args
         L.rrt_scene_file_load.argtypes = [C.c_char_p, C.POINTER(vp)]
@@ -366,6 +366,19 @@ class Renderer:
         geom = np.zeros(5, np.float64)
         self._chk(0 if lib().rrt_get_free_grid(self.h, _p(k), _p(geom), _p(n)) > 0 else RRT_E_INVALID)
         return k, geom[:3].copy(), float(geom[3]), float(geom[4])
+
+    def big_masks(self):
+        """(mask [nz][ny][nx] uint32 over the free grid's cells, reach) of the oversized-leaf masks, or None."""
+        cells = lib().rrt_get_big_masks(self.h, None, None)
+        if cells < 0:
+            raise RRTError(cells, "no scene")
+        if cells == 0:
+            return None
+        g = self.free_grid()
+        m = np.zeros(g[0].shape, np.uint32)
+        reach = np.zeros(1, np.float64)
+        lib().rrt_get_big_masks(self.h, _p(m), _p(reach))
+        return m, float(reach[0])
 
     def clean_tree(self):
         """(boxes [n,6], nodes [n,4] (skip, first, count, ordinal), big_boxes [nb,6], big [nb,3]

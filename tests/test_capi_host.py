@@ -200,6 +200,53 @@ def test_free_grid_is_conservative(host_ctx, scene):
 
 
 @pytest.mark.parametrize("scene", ["CBbunny", "CBcoil", "CBgems"])
+def test_big_leaf_masks_are_conservative(host_ctx, scene):
+    """Oversized-leaf masks: where a cell's bit for oversized leaf b is clear,
+    every point of the cell is at least `reach` from every primitive of b, so a segment shorter
+    than reach that starts there cannot be accepted by them and the walk may skip b."""
+    path = os.path.join(GOLD, "scenes", scene + ".rrts")
+    host_ctx.set_scene(rrt.SceneFile(path))
+    bm = host_ctx.big_masks()
+    assert bm is not None
+    mask, reach = bm
+    k, g0, inv_h, h_free = host_ctx.free_grid()
+    assert mask.shape == k.shape and abs(reach - (rrt_internal_reach() - 1) * h_free) < 1e-15
+    _, _, _, big = host_ctx.clean_tree()
+    _, _, leaf_prims = host_ctx.bvh()
+    tris, sph = _scene_prims(path)
+    assert len(sph) == 0
+    rng = np.random.default_rng(11)
+    n = np.array(k.shape[::-1])
+    span = n / inv_h
+    pts = g0 + rng.uniform(-0.02, 1.02, size=(1500, 3)) * span
+    t = tris[rng.integers(0, len(tris), 1500)]
+    wts = rng.dirichlet([1, 1, 1], 1500)
+    pts = np.concatenate([pts, (wts[:, :, None] * t).sum(1) + rng.normal(0, 12 / inv_h, (1500, 3))])
+    f = (pts - g0) * inv_h                       # same arithmetic as grid_cell()
+    inside = np.all((f >= 0) & (f < n), axis=1)
+    pts, f = pts[inside], f[inside]
+    idx = f.astype(np.int64)
+    m = mask[idx[:, 2], idx[:, 1], idx[:, 0]]
+    skipped = 0
+    for b, (first, count, _) in enumerate(big):
+        clear = (m >> np.uint32(b)) & 1 == 0
+        if not clear.any():
+            continue
+        bt = tris[leaf_prims[first:first + count]]
+        p = pts[clear][:, None, :]
+        d = _tri_dist(p, bt[None, :, 0], bt[None, :, 1], bt[None, :, 2]).min(1)
+        assert d.min() >= reach, (b, d.min(), reach)
+        skipped += int(clear.sum())
+    assert skipped > 0.3 * len(pts) * len(big)  # the masks do cull most leaves
+
+
+def rrt_internal_reach():
+    import re
+    src = open(os.path.join(os.path.dirname(rrt.__file__), "csrc", "rrt_internal.h")).read()
+    return int(re.search(r"#define RRT_BIG_REACH (\d+)", src).group(1))
+
+
+@pytest.mark.parametrize("scene", ["CBbunny", "CBcoil", "CBgems"])
 def test_clean_walk_matches_reference_walk(host_ctx, scene):
     """The clean-tree walk (oversized leaves listed apart, inner boxes refit), with and without the
     plane cull in front of primitive tests, returns the same closest hit (leaf slot and t, bit for

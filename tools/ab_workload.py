@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B kernel variants (rrt_render_params.variant = waves per SIMD, flags) on a bench.py workload,
 interleaved rounds in one process; prints the HIP-event kernel time per variant.
-Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5"""
+Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT or VARIANT:FLAGS)"""
 import argparse
 import json
 import os
@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg5", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("variants", type=int, nargs="+")
+    ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
     W, H, ts = wl["w"], wl["h"], 32
@@ -41,13 +41,14 @@ def main():
     times, sums = {v: [] for v in a.variants}, {}
     for _ in range(a.rounds):
         for v in a.variants:
-            p = rrt.render_params(W, H, ns_aa=wl["spp"], variant=v)
+            var, _, fl = v.partition(":")
+            p = rrt.render_params(W, H, ns_aa=wl["spp"], variant=int(var), flags=int(fl or 0))
             r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
             torch.cuda.synchronize()
             times[v].append(r.stats().last_kernel_ms)
             sums[v] = (float(prgb.double().sum().item()), int(pcnt.long().sum().item()))
             print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
-    same = len(set(sums.values())) == 1
+    same = len(set(s for v, s in sums.items() if ":" not in v)) <= 1  # diagnostic flags change outputs
     print(json.dumps({"workload": a.workload, "identical_outputs": same,
                       "median_ms": {v: float(np.median(t)) for v, t in times.items()}}))
 
