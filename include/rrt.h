@@ -170,6 +170,11 @@ enum {
                                      of centre-first (A/B testing) */
   RRT_RENDER_NO_FIRST = 1u << 10, /* sample-parallel kernel: no sample-0 pre-pass (speculate
                                      "miss" for a pixel's first step; A/B testing) */
+  RRT_RENDER_ONE_QUEUE = 1u << 11, /* sample-parallel kernel: one chip-wide claim queue (A/B
+                                     testing; results are identical) */
+  RRT_RENDER_XCD_QUEUES = 1u << 12, /* sample-parallel kernel: one claim queue per XCD (A/B
+                                     testing; results are identical).  Default: per-XCD queues
+                                     for the general and Kerr builds, one queue for LEAN builds */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of

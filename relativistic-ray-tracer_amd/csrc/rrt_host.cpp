@@ -35,6 +35,7 @@ hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float
 namespace {
 
 constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
+constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;  // claim counters
 
 struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
@@ -192,7 +193,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
+        hipMalloc(&c->d_counter, kCounterBytes) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
       return RRT_E_HIP;
     }
@@ -876,7 +877,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     c->tiles_cap = n_tiles;
   }
   HIPCHK(c, hipMemcpyAsync(c->d_tiles, tiles, sizeof(uint32_t) * 2 * n_tiles, hipMemcpyHostToDevice, stream));
-  HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 64, stream));
+  HIPCHK(c, hipMemsetAsync(c->d_counter, 0, kCounterBytes, stream));
   KParams kp{};
   kp.nodes = c->d_nodes; kp.geo = c->d_geo; kp.nrm = c->d_nrm; kp.meta = c->d_meta;
   kp.bsdfs = c->d_bsdfs; kp.lights = c->d_lights; kp.n_lights = (uint32_t)c->lights.size() + (c->env_w ? 1u : 0u);
@@ -975,17 +976,40 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // Claim order: tiles nearest the frame centre first (where the geometry and the black hole's
     // ring usually are), so the launch ends on cheap border tiles rather than on a costly
     // region; consecutive claims stay spatially adjacent (coherent waves, warm caches).
+    // One queue per XCD (workgroups are dealt to the 8 XCDs round-robin, so block b starts on
+    // queue b % 8): queue q holds the tiles of the q-th 45-degree sector about the frame centre,
+    // centre-first.  Each XCD's L2 then serves a coherent wedge of the frame (a narrower slice
+    // of the BVH), every wedge gets its share of the costly centre, and a block whose queue is
+    // empty moves on to the next queue, so the load still balances at pixel granularity.
     std::vector<uint32_t> order(n_tiles);
     for (uint32_t k = 0; k < n_tiles; ++k) order[k] = k;
-    if (!(p->flags & RRT_RENDER_ORDERED)) {
+    const bool ordered = p->flags & RRT_RENDER_ORDERED;
+    // A/B (profiles/r01_queues_ab.md): per-XCD queues cost the LEAN cfg3 build 6% and save the
+    // Kerr cfg5 build 2%, so they are the default for the general / Kerr builds only
+    const bool xcd_q = (p->flags & RRT_RENDER_XCD_QUEUES) || ((lean == 0 || lean == 3) && !(p->flags & RRT_RENDER_ONE_QUEUE));
+    const uint32_t nq = (ordered || !xcd_q) ? 1u : RRT_MAX_QUEUES;
+    std::vector<uint32_t> sector(n_tiles, 0);
+    if (!ordered) {
       const double cx = 0.5 * p->frame_w, cy = 0.5 * p->frame_h;
       std::vector<double> key(n_tiles);
       for (uint32_t k = 0; k < n_tiles; ++k) {
         const double dx = tiles[2 * k] + 0.5 * ts - cx, dy = tiles[2 * k + 1] + 0.5 * ts - cy;
         key[k] = dx * dx + dy * dy;
+        if (nq > 1) {
+          const double a = std::atan2(dy, dx) + kPI;  // [0, 2 pi]
+          sector[k] = std::min<uint32_t>((uint32_t)(a * (nq / (2 * kPI))), nq - 1);
+        }
       }
-      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return sector[a] != sector[b] ? sector[a] < sector[b] : key[a] < key[b];
+      });
     }
+    kp.n_queues = nq;
+    for (uint32_t q = 0, k = 0; q < RRT_MAX_QUEUES; ++q) {
+      while (k < n_tiles && sector[order[k]] == q) ++k;
+      kp.q_end[q] = q < nq ? k * ts * ts : kp.n_pixels;
+    }
+    kp.q_end[nq - 1] = kp.n_pixels;
     if (c->order_cap < n_tiles) {
       hipFree(c->d_order); c->d_order = nullptr;
       HIPCHK(c, hipMalloc(&c->d_order, sizeof(uint32_t) * n_tiles));

@@ -97,6 +97,9 @@ struct DGrid {
   int32_t pad;
 };
 
+#define RRT_MAX_QUEUES 8
+#define RRT_QUEUE_STRIDE 16  // counters 64 B apart
+
 struct KParams {
   // scene
   const DNode* nodes;
@@ -137,6 +140,10 @@ struct KParams {
   // sample-parallel kernel (rrt_sample.hip rrt_batch_kernel)
   uint32_t n_pixels;     // n_tiles * tile_size^2 (pixel work items)
   const uint32_t* tile_order;  // claim order over the caller's tile list
+  // claim queues (one per XCD): queue q holds claim indices [q_end[q-1], q_end[q]) of tile_order,
+  // its counter is block_counter[RRT_QUEUE_STRIDE * q]; a block starts on queue blockIdx % n_queues
+  uint32_t n_queues;
+  uint32_t q_end[RRT_MAX_QUEUES];
   struct FirstSample { float r, g, b; uint32_t hit; };
   FirstSample* first;          // sample 0 of every pixel slot (rrt_first_kernel), or null
   uint32_t group;        // lanes per pixel (power of two, 2..32)

@@ -327,12 +327,21 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 #endif
 
   bool have = false, done = false;
+  uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
 
   for (;;) {
     // ---- claim a pixel (one atomic per group)
     if (!have && !done) {
       uint32_t p = 0;
-      if (gl == 0) p = atomicAdd(kp.block_counter, 1u);
+      if (gl == 0) {  // this XCD's queue first, then the others in turn (KParams::q_end)
+        for (;;) {
+          const uint32_t qb = q ? kp.q_end[q - 1] : 0u;
+          const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, 1u);
+          if (k < kp.q_end[q] - qb) { p = qb + k; break; }
+          if (--q_left == 0) { p = kp.n_pixels; break; }
+          q = q + 1 == kp.n_queues ? 0u : q + 1;
+        }
+      }
       p = __shfl(p, (int)gbase);
       if (p >= kp.n_pixels) {
         done = true;

@@ -28,7 +28,8 @@ KERR_CASES = [
     ("glass_mirror_96x72_s16_m4", 0.7, (0.0, 1.0, 0.0)),
 ]
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
-            "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP}
+            "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
+            "onequeue": rrt.RRT_RENDER_ONE_QUEUE}
 _oracle_cache = {}
 
 

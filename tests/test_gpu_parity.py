@@ -52,8 +52,11 @@ def check(c, rgb, cnt, draws):
 
 # every kernel path must meet the same bar: default (sample-parallel kernel, clean-tree BVH walk,
 # empty-space grid), the reference-tree walk without the grid, the lane-per-pixel per-sample
-# kernel, the per-pixel-loop kernel and the wavefront state-machine kernel
+# kernel, the per-pixel-loop kernel and the wavefront state-machine kernel; the sample-parallel
+# kernel also with one chip-wide claim queue, one queue per XCD, and in list order
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
+            "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "xcdqueues": rrt.RRT_RENDER_XCD_QUEUES,
+            "ordered": rrt.RRT_RENDER_ORDERED,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "wavefront": rrt.RRT_RENDER_WAVEFRONT}
 
