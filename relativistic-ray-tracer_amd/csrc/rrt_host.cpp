@@ -26,7 +26,7 @@ hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, i
 hipError_t rrt_launch_mega(const KParams& kp, const KParams* d_kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
-hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -1047,10 +1047,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
     const int w = lean == 1 ? bw : lean == 2 ? (bw >= 3 && bw <= 6 ? bw : 5) : gw;
     char first[32] = "";
-    if (kp.first) std::snprintf(first, sizeof(first), "rrt_first_kernel<%d> + ", lean);
+    const uint32_t fwv = (p->variant >> 8) & 0xfu;  // pre-pass waves/SIMD (A/B), default 3
+    const int fw = (lean == 1 && (fwv == 4 || fwv == 5)) ? (int)fwv : 3;
+    if (kp.first) std::snprintf(first, sizeof(first), "rrt_first_kernel<%d, %d> + ", lean, fw);
     std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%d, %d>", first, lean, w);
     if (kp.first)
-      HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
+      HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, fw, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
   } else if (mega) {

@@ -508,8 +508,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 // tile).  Its draw offset is always 0, so it needs no speculation; its hit status then seeds the
 // batch kernel's hypothesis for the pixel's other samples (all-hit and all-miss pixels -- 99.9%
 // of cfg3 -- then need a single round), and its radiance is the first term of the pixel's sums.
-template <int LEAN>
-__global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __restrict__ kpp) {
+template <int LEAN, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void rrt_first_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
   __shared__ ShadeLds cl;
@@ -546,11 +546,14 @@ __global__ __launch_bounds__(256, 3) void rrt_first_kernel(const KParams* __rest
   }
 }
 
-hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, uint32_t grid, hipStream_t stream) {
-  if (lean == 1) hipLaunchKernelGGL((rrt_first_kernel<1>), dim3(grid), dim3(256), 0, stream, d_kp);
-  else if (lean == 2) hipLaunchKernelGGL((rrt_first_kernel<2>), dim3(grid), dim3(256), 0, stream, d_kp);
-  else if (lean == rrt::V_KERR) hipLaunchKernelGGL((rrt_first_kernel<rrt::V_KERR>), dim3(grid), dim3(256), 0, stream, d_kp);
-  else hipLaunchKernelGGL((rrt_first_kernel<0>), dim3(grid), dim3(256), 0, stream, d_kp);
+hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
+  // waves/SIMD: 3 by default; the LEAN area-light build also at 4 / 5 (A/B)
+  if (lean == 1 && waves == 4) hipLaunchKernelGGL((rrt_first_kernel<1, 4>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == 1 && waves == 5) hipLaunchKernelGGL((rrt_first_kernel<1, 5>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == 1) hipLaunchKernelGGL((rrt_first_kernel<1, 3>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == 2) hipLaunchKernelGGL((rrt_first_kernel<2, 3>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else if (lean == rrt::V_KERR) hipLaunchKernelGGL((rrt_first_kernel<rrt::V_KERR, 3>), dim3(grid), dim3(256), 0, stream, d_kp);
+  else hipLaunchKernelGGL((rrt_first_kernel<0, 3>), dim3(grid), dim3(256), 0, stream, d_kp);
   return hipGetLastError();
 }
 
