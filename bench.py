@@ -118,8 +118,9 @@ def main():
     ap.add_argument("--variant", type=int, default=0, help="rrt_render_params.variant (A/B: waves per SIMD)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
-                    help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic; "
+                         "default profiles/r01_traffic.json (cfg3) or profiles/r01_traffic_<workload>.json")
     a = ap.parse_args()
 
     import torch
@@ -224,7 +225,10 @@ def main():
     loc_bytes = BYTES_AABB * xc4[0] + BYTES_PRIM * xc4[2] + BYTES_PLANE * xc4[3] + BYTES_PIXEL * pix_local
     ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
     traffic = None
-    if a.traffic and os.path.exists(a.traffic):
+    if a.traffic is None:
+        a.traffic = os.path.join(ROOT, "profiles", "r01_traffic.json" if a.workload == "cfg3"
+                                 else f"r01_traffic_{a.workload}.json")
+    if os.path.exists(a.traffic):
         with open(a.traffic) as f:
             tr = json.load(f)
         if tr.get("workload") == a.workload and tr.get("kernel") == kernel_name:
