@@ -203,7 +203,10 @@ int rrt_render(rrt_ctx* ctx, const rrt_render_params* p, uint32_t x0, uint32_t y
  * the frame) into PACKED device buffers: pixel (i, j) of list entry t goes to
  * rgb[(t * tile_size * tile_size + j * tile_size + i) * 3], count[...] likewise.  Asynchronous
  * on `stream` (a hipStream_t, NULL = default stream); no host synchronisation.
- * tiles is a host array of 2*n_tiles uint32. */
+ * tiles is a host array of 2*n_tiles uint32.  A context owns one launch workspace (parameters,
+ * claim counters, tile list): a launch or unpack on a different stream than the context's
+ * previous one makes its stream wait for that previous use first (hipStreamWaitEvent), so
+ * launches of one context never overlap; use one context per stream to overlap renders. */
 int rrt_render_tiles_device(rrt_ctx* ctx, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles,
                             uint32_t tile_size, float* d_rgb, int32_t* d_count, uint32_t* d_counters,
                             void* stream);

@@ -83,6 +83,12 @@ struct rrt_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // scratch fence: every launch and unpack rewrites the per-context workspace below (KParams,
+  // claim counters, tile list/order, sample-0 slots) with async copies on the caller's stream;
+  // a use on a different stream than the previous one first waits for this event
+  hipEvent_t ev_fence = nullptr;
+  hipStream_t fence_stream = nullptr;
+  bool fenced = false;
   int n_cu = 256;
   // host scene
   std::vector<V3> pos, nrm;
@@ -193,6 +199,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counter, kCounterBytes) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
       return RRT_E_HIP;
@@ -213,6 +220,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipFree(c->d_ctr);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->ev_fence) hipEventDestroy(c->ev_fence);
     if (c->stream) hipStreamDestroy(c->stream);
   }
   delete c;
@@ -561,6 +569,10 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if (s->n_objects && !s->objects) return fail(c, RRT_E_INVALID, "objects missing");
   if (s->n_bsdfs && !s->bsdfs) return fail(c, RRT_E_INVALID, "bsdfs missing");
   if (s->n_lights && !s->lights) return fail(c, RRT_E_INVALID, "lights missing");
+  // a failed set_scene leaves no scene: rrt_render then fails with RRT_E_INVALID instead of
+  // reading the emptied host tables or the previous scene's device buffers
+  c->has_scene = false;
+  c->has_clean = false;
   c->pos.clear(); c->nrm.clear(); c->prims.clear(); c->nodes.clear(); c->leaf.clear(); c->max_depth = 0;
   c->bsdfs.assign(s->n_bsdfs, DBsdf{});
   for (uint32_t i = 0; i < s->n_bsdfs; ++i) {
@@ -700,8 +712,10 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     if (l.type != RRT_LIGHT_AREA && l.type != RRT_LIGHT_POINT) c->lean = 0;
   }
   for (const DBsdf& b : c->bsdfs) if (b.type == RRT_BSDF_MICROFACET) c->lean = 0;
-  c->has_scene = true;
-  if (c->device < 0) return RRT_OK;
+  if (c->device < 0) {
+    c->has_scene = true;
+    return RRT_OK;
+  }
   HIPCHK(c, hipSetDevice(c->device));
   free_scene_dev(c);
   int rc;
@@ -720,6 +734,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
         (rc = upload(c, (void**)&c->d_big_mask, c->big_mask.data(), c->big_mask.size() * sizeof(uint32_t))))
       return rc;
   }
+  c->has_scene = true;
   return RRT_OK;
 }
 
@@ -859,6 +874,19 @@ static int ensure(rrt_ctx* c, void** p, size_t& cap, size_t need, size_t elem) {
   return RRT_OK;
 }
 
+// Order this use of the context's workspace after the previous one when the streams differ
+// (same-stream uses are ordered by the stream itself).
+static int scratch_acquire(rrt_ctx* c, hipStream_t stream) {
+  if (c->fenced && c->fence_stream != stream) HIPCHK(c, hipStreamWaitEvent(stream, c->ev_fence, 0));
+  return RRT_OK;
+}
+static int scratch_release(rrt_ctx* c, hipStream_t stream) {
+  HIPCHK(c, hipEventRecord(c->ev_fence, stream));
+  c->fence_stream = stream;
+  c->fenced = true;
+  return RRT_OK;
+}
+
 static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles, uint32_t ts,
                   uint32_t cx0, uint32_t cy0, uint32_t cx1, uint32_t cy1, float* d_rgb, int32_t* d_cnt,
                   uint32_t* d_draws, uint32_t* d_ctr, hipStream_t stream) {
@@ -871,7 +899,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (ts == 0 || ts % 8 != 0) return fail(c, RRT_E_INVALID, "tile_size must be a positive multiple of 8");
   if (n_tiles == 0) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = scratch_acquire(c, stream)) return rc;
   if (c->tiles_cap < n_tiles) {
+    // hipFree waits for the device, so no launch still reads the old list
     hipFree(c->d_tiles); c->d_tiles = nullptr;
     HIPCHK(c, hipMalloc(&c->d_tiles, sizeof(uint32_t) * 2 * n_tiles));
     c->tiles_cap = n_tiles;
@@ -1068,7 +1098,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   c->last_kernel = name;
   HIPCHK(c, hipEventRecord(c->ev1, stream));
   c->timed = true;
-  return RRT_OK;
+  return scratch_release(c, stream);
 }
 
 extern "C" int rrt_render_tiles_device(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
@@ -1086,6 +1116,7 @@ extern "C" int rrt_unpack_tiles_device(rrt_ctx* c, const uint32_t* tiles, uint32
   if (n_tiles == 0) return RRT_OK;
   hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)0;
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = scratch_acquire(c, s)) return rc;
   if (c->tiles_cap < n_tiles) {
     hipFree(c->d_tiles); c->d_tiles = nullptr;
     HIPCHK(c, hipMalloc(&c->d_tiles, sizeof(uint32_t) * 2 * n_tiles));
@@ -1093,7 +1124,7 @@ extern "C" int rrt_unpack_tiles_device(rrt_ctx* c, const uint32_t* tiles, uint32
   }
   HIPCHK(c, hipMemcpyAsync(c->d_tiles, tiles, sizeof(uint32_t) * 2 * n_tiles, hipMemcpyHostToDevice, s));
   HIPCHK(c, rrt_launch_unpack(c->d_tiles, n_tiles, ts, fw, fh, rgb_p, cnt_p, rgb, cnt, s));
-  return RRT_OK;
+  return scratch_release(c, s);
 }
 
 extern "C" int rrt_tonemap_device(rrt_ctx* c, uint32_t n, const float* rgb, uint32_t* rgba, void* stream) {

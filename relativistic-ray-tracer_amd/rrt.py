@@ -180,6 +180,11 @@ class SceneFile:
         if rc != RRT_OK:
             raise RRTError(rc, f"cannot write {path}")
 
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rrt_scene_file_free(self.h)
+            self.h = None
+
 
 def load_collada(path, screen_w=800, screen_h=600, lens_radius=0.25, focal_distance=4.7):
     """Native COLLADA ingest: (SceneFile, CameraState) as the reference's loader + Application::load
@@ -221,11 +226,6 @@ def load_camera_state(path):
     if rc != RRT_OK:
         raise RRTError(rc, f"cannot load camera {path}")
     return st
-
-    def __del__(self):
-        if getattr(self, "h", None) and _lib is not None:
-            _lib.rrt_scene_file_free(self.h)
-            self.h = None
 
 
 def load_camera(path):

@@ -101,6 +101,33 @@ def test_errors(host_ctx):
     assert rrt.lib().rrt_set_spacetime(host_ctx.h, C.byref(st)) == rrt.RRT_E_INVALID
 
 
+class _SceneDescHead(C.Structure):  # include/rrt.h rrt_scene_desc
+    _fields_ = [("n_objects", C.c_uint32), ("n_bsdfs", C.c_uint32), ("n_lights", C.c_uint32),
+                ("reserved", C.c_uint32), ("objects", C.c_void_p), ("bsdfs", C.c_void_p), ("lights", C.c_void_p)]
+
+
+def _bad_scene_after_good(ctx):
+    """Load a valid scene, then a desc whose objects name BSDFs that do not exist: the second
+    rrt_set_scene must fail and leave the context with NO scene (not the first one's device
+    buffers paired with the emptied host tables)."""
+    sf = rrt.SceneFile(os.path.join(GOLD, "scenes", "CBspheres_lambertian.rrts"))
+    ctx.set_scene(sf)
+    good = _SceneDescHead.from_address(sf.desc())
+    bad = _SceneDescHead(good.n_objects, 0, good.n_lights, 0, good.objects, None, good.lights)
+    assert rrt.lib().rrt_set_scene(ctx.h, C.byref(bad)) == rrt.RRT_E_INVALID
+    return sf
+
+
+def test_failed_set_scene_leaves_no_scene():
+    r = rrt.Renderer(device=-1)
+    try:
+        _bad_scene_after_good(r)
+        assert rrt.lib().rrt_get_bvh(r.h, None, None, None) == rrt.RRT_E_INVALID
+        assert rrt.lib().rrt_get_clean_tree(r.h, None, None, None, None) == rrt.RRT_E_INVALID
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("kind,r_s,spin,ok", [(1, 0.1, 0.0, True), (1, 0.1, 0.999, True), (1, 0.1, 1.0, False),
                                               (1, 0.1, -0.1, False), (1, 0.0, 0.5, False), (2, 0.1, 0.5, False),
                                               (0, 0.1, 7.0, True)])

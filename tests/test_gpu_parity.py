@@ -132,3 +132,58 @@ def test_tonemap(gpu):
     want = 0xFF000000 | (q[..., 2] << 16) | (q[..., 1] << 8) | q[..., 0]
     diff = np.abs(((got >> 0) & 255).astype(int) - (want & 255).astype(int))
     assert diff.max() <= 1 and np.mean(got == want) > 0.999
+
+
+def test_render_after_failed_set_scene():
+    """A failed second rrt_set_scene leaves no scene: rrt_render reports RRT_E_INVALID instead of
+    launching over the previous scene's device buffers."""
+    from test_capi_host import _bad_scene_after_good
+
+    r = rrt.Renderer(device=0)
+    try:
+        _bad_scene_after_good(r)
+        r.set_camera(rrt.load_camera(Case("spheres_96x72_s1").camera_path))
+        with pytest.raises(rrt.RRTError) as e:
+            r.render(rrt.render_params(16, 16), 0, 0, 16, 16)
+        assert e.value.code == rrt.RRT_E_INVALID
+    finally:
+        r.close()
+
+
+def test_two_streams_one_context(gpu):
+    """rrt_render_tiles_device on two streams of one context: the second launch waits for the
+    first (the context's workspace is fenced), so both frames equal the golden one."""
+    import torch
+
+    c = Case("spheres_96x72_s8_l4")
+    assert c.exact
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(None)
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    bh = c.cfg["bh"]
+    gpu.set_black_hole(bh[:3], bh[3], bh[4])
+    g = c.cfg
+    p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                          ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                          max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"])
+    ts = 32
+    tiles = np.array([(x, y) for y in range(0, c.frame_h, ts) for x in range(0, c.frame_w, ts)], np.uint32)
+    n = len(tiles) * ts * ts
+    outs = []
+    streams = [torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)]
+    for s in streams:
+        rgb = torch.empty(n * 3, dtype=torch.float32, device="cuda:0")
+        cnt = torch.empty(n, dtype=torch.int32, device="cuda:0")
+        gpu.render_tiles_device(p, tiles, ts, rgb.data_ptr(), cnt.data_ptr(), stream=s.cuda_stream)
+        outs.append((rgb, cnt))
+    torch.cuda.synchronize()
+    frames = []
+    for rgb, cnt in outs:
+        fr = np.zeros((c.frame_h, c.frame_w, 3), np.float32)
+        rg = rgb.cpu().numpy().reshape(len(tiles), ts, ts, 3)
+        for t, (x, y) in enumerate(tiles):
+            h, w = min(ts, c.frame_h - y), min(ts, c.frame_w - x)
+            fr[y:y + h, x:x + w] = rg[t, :h, :w]
+        frames.append(fr[c.y0:c.y0 + c.h, c.x0:c.x0 + c.w])
+    assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
+    assert np.array_equal(frames[0].view(np.uint32), c.px["rgb"].view(np.uint32))
