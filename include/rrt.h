@@ -175,6 +175,9 @@ enum {
   RRT_RENDER_XCD_QUEUES = 1u << 12, /* sample-parallel kernel: one claim queue per XCD (A/B
                                      testing; results are identical).  Default: per-XCD queues
                                      for the general and Kerr builds, one queue for LEAN builds */
+  RRT_RENDER_NO_MISS_PROOF = 1u << 13, /* march every camera ray exactly instead of first trying
+                                     the planar-recurrence miss proof (A/B testing; results
+                                     are identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of

@@ -134,7 +134,7 @@ __device__ __forceinline__ v3 hemisphere_sample(Rng& g) {  // sampler.cpp:15-29 
 struct Counters {
   uint32_t bbox, micro, prim, query;
 #if RRT_PROFILE
-  uint64_t t_micro, t_trav, t_query;
+  uint64_t t_micro, t_trav, t_query, t_proof, t_squery, t_strav;
 #endif
 };
 #if RRT_PROFILE
@@ -441,9 +441,12 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
 // div_core, qdiv) and `ok` collects whether all operands were in the core's exact range; the
 // caller re-runs the step with IEEE operations when one was not (rare: zero / tiny / huge
 // operands), so the result is always the IEEE one without a range branch per operation.
+// The step's planar state (the camera-ray miss proof starts from step 0's): orbital-plane basis
+// x_axis, y_axis, u and u' before the update, and the updated u (v).
+struct MicroOut { v3 x, y; double u, up, v; };
 template <bool FAST>
 __device__ __forceinline__ void next_micro_impl(const DHole& h, v3 no, v3& o, v3& d, double& max_t, v3& rel,
-                                                double& rel2, bool& ok) {
+                                                double& rel2, bool& ok, MicroOut* mo = nullptr) {
   auto SQ = [&](double x) -> double {
     if (!FAST) return sqrt(x);
     ok = ok && in_core_range(x);
@@ -482,7 +485,9 @@ __device__ __forceinline__ void next_micro_impl(const DHole& h, v3 no, v3& o, v3
   double f2 = -u2 + k * u2 * u2 / 2.0;
   double u3 = u + up * dt / 2.0 + f1 * dt * dt / 4.0;
   double f3 = -u3 + k * u3 * u3 / 2.0;
+  if (mo) { mo->x = x_axis; mo->y = y_axis; mo->u = u; mo->up = up; }
   u += up * dt + D6((f1 + f2 + f3) * dt * dt);
+  if (mo) mo->v = u;
   double dd = RC(u);
   double next_x = dd * h.cos_dt, next_y = dd * h.sin_dt;
   v3 nd = ((V(h.c[0], h.c[1], h.c[2]) + smul(next_x, x_axis)) + smul(next_y, y_axis)) - no;
@@ -495,17 +500,17 @@ __device__ __forceinline__ void next_micro_impl(const DHole& h, v3 no, v3& o, v3
 // same value the reference computes at blackhole.cpp:18); rel = no - c and rel2 = |rel|^2 are
 // also the capture test's o - c and |o - c|^2 (sphere.cpp:12-14 on the new segment).
 __device__ __forceinline__ void next_micro_at(const DHole& h, v3 no, v3& o, v3& d, double& max_t, v3& rel,
-                                              double& rel2) {
+                                              double& rel2, MicroOut* mo = nullptr) {
   bool ok = true;
   if (RRT_LIBM_DIVSQRT) {
-    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok);
+    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok, mo);
     return;
   }
   const v3 d0 = d;
-  next_micro_impl<true>(h, no, o, d, max_t, rel, rel2, ok);
+  next_micro_impl<true>(h, no, o, d, max_t, rel, rel2, ok, mo);
   if (__builtin_expect(!ok, 0)) {  // some operand outside the core's range: the IEEE step
     d = d0;
-    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok);
+    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok, mo);
   }
 }
 __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double& max_t) {
@@ -552,7 +557,9 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   else
     hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
-  RRT_ACC(t_trav, tt0);
+#if RRT_PROFILE
+  if (ANY) cn.t_strav += clock64() - tt0; else cn.t_trav += clock64() - tt0;
+#endif
   if (COUNT && (kp.diag & 2)) cn.prim = prim_before + (clear_diag ? 0u : cn.bbox - bbox_before);
   if (!hit) return false;
   if (!ANY) {
@@ -756,6 +763,11 @@ __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect*
 // incoming ray's min_t / max_t are dropped (camera clip planes and shadow-ray distance are
 // ignored, as in the reference).  Capture by the hole returns "no hit".  KERR: the Kerr build
 // of the kernel (kernel variant V_KERR, chosen by rrt_host.cpp launch() for a Kerr spacetime).
+#if RRT_PROFILE
+#define RRT_QACC(v) do { if (ANY) cn.t_squery += clock64() - v; else cn.t_query += clock64() - v; } while (0)
+#else
+#define RRT_QACC(v)
+#endif
 template <bool ANY, bool COUNT, bool KERR = false>
 __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   if (KERR) return query_kerr<ANY, COUNT>(kp, o, d, is, cn);
@@ -771,17 +783,114 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
     RRT_ACC(t_micro, tm0);
     if (COUNT) cn.micro++;
     if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) {  // captured
-      RRT_ACC(t_query, tq0);
+      RRT_QACC(tq0);
       return false;
     }
     e = o + vmul(d, max_t);
     if (segment_query<ANY, COUNT>(kp, o, d, max_t, e, is, cn)) {
-      RRT_ACC(t_query, tq0);
+      RRT_QACC(tq0);
       return true;
     }
   }
-  RRT_ACC(t_query, tq0);
+  RRT_QACC(tq0);
   return false;
+}
+
+// ------------------------------------------------------------------ camera-ray miss proof
+// (DESIGN.md §5 "Miss proof").  In exact arithmetic the reference's march (next_micro_ray) is
+// planar about the hole and reduces to a scalar recurrence: with s = u at a step's start, u' its
+// derivative and v the updated u, the step places the next point at c + (cos dt x + sin dt y) / v
+// (flipped through the hole when v < 0), and the next step starts from
+//   s' = |v| / rho,   u'' = (v cos dt / rho - rho s) / sin dt,   rho = |(cos dt, sin dt)|,
+// its x axis = sign(v) E and its y axis = E rotated a quarter turn the same way as y from x,
+// E = (cos dt x + sin dt y) / rho.  The reference's floating-point march stays within a relative
+// 1e-12 / kappa of that recurrence while no step cancels (|v| >= kappa (|s| + |u' dt|)) --
+// measured over 3e5 rays per BASELINE scene (tools/miss_proof_check.py) and on the GPU
+// (tests/test_gpu_parity.py) -- so a segment of the recurrence that misses the root box widened
+// by eta (|P - c| + scale), eta >= 1e3 x that bound, is a reference segment whose root slab test
+// fails.  If every segment misses, the reference's query returns "no hit" (captured or not), so
+// the camera ray is a miss without the exact march.  Step 0 is the reference's own step (bit
+// exact) and its segment takes the reference's root test.  Any doubt (a cancelling step, a
+// segment near the box, NaN) returns false: the caller marches the ray exactly.
+__device__ __forceinline__ bool seg_clear_of_box(v3 a, v3 b, const double* lo, const double* hi, double m) {
+#pragma clang fp contract(fast)
+  const double l0 = lo[0] - m, l1 = lo[1] - m, l2 = lo[2] - m, h0 = hi[0] + m, h1 = hi[1] + m, h2 = hi[2] + m;
+  if (fmax(a.x, b.x) < l0 || fmin(a.x, b.x) > h0 || fmax(a.y, b.y) < l1 || fmin(a.y, b.y) > h1 ||
+      fmax(a.z, b.z) < l2 || fmin(a.z, b.z) > h2)
+    return true;
+  // slab test of the segment a + t (b - a), t in [0, 1]; every axis overlaps the widened box here,
+  // so an axis with no extent along the segment constrains nothing
+  const double dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+  double tmin = 0.0, tmax = 1.0;
+  if (dx != 0.0) { const double i = 1.0 / dx, t0 = (l0 - a.x) * i, t1 = (h0 - a.x) * i; tmin = fmax(tmin, fmin(t0, t1)); tmax = fmin(tmax, fmax(t0, t1)); }
+  if (dy != 0.0) { const double i = 1.0 / dy, t0 = (l1 - a.y) * i, t1 = (h1 - a.y) * i; tmin = fmax(tmin, fmin(t0, t1)); tmax = fmin(tmax, fmax(t0, t1)); }
+  if (dz != 0.0) { const double i = 1.0 / dz, t0 = (l2 - a.z) * i, t1 = (h2 - a.z) * i; tmin = fmax(tmin, fmin(t0, t1)); tmax = fmin(tmax, fmax(t0, t1)); }
+  return tmin > tmax + 1e-9;  // NaN: not clear
+}
+template <bool COUNT = false>
+__device__ __forceinline__ bool camera_miss_proof(const KParams& kp, v3 o, v3 d, Counters& cn) {
+  const DMissProof& mp = kp.miss;
+  const DHole& h = kp.hole;
+  // step 0: the reference's own step from the camera ray (bit exact) and its root slab test
+  MicroOut m0;
+  v3 rel;
+  double rel2, max_t = 0.0;
+  next_micro_at(h, o + vmul(d, max_t), o, d, max_t, rel, rel2, &m0);
+  const v3 e = o + vmul(d, max_t);
+  if (!segment_outside_root(kp, o, e)) {
+    const v3 y = V(xdiv(1.0, d.x), xdiv(1.0, d.y), xdiv(1.0, d.z));
+    if (COUNT) cn.bbox++;
+    if (slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, !segment_fast(kp, o, d))) return false;
+  }
+  {
+#pragma clang fp contract(fast)
+    const v3 c = V(h.c[0], h.c[1], h.c[2]);
+    const v3 X = m0.x, Y = m0.y;
+    double s = m0.u, up = m0.up, vprev = m0.v;
+    double ea = mp.co1, eb = mp.si1, sig = 1.0;  // E of the point just placed, in (X, Y); sense of y from x
+    v3 pp = e;
+    double rp = sqrt(norm2(e - c));
+    for (int j = 1; j < h.steps; ++j) {
+      // the next step's start: s, u', and its frame (x = sg E, y = E turned by sig)
+      const double sg = vprev < 0.0 ? -1.0 : 1.0;
+      up = (vprev * mp.co1 - mp.rho * s) * mp.inv_si;
+      s = fabs(vprev) * mp.inv_rho;
+      // blackhole.cpp:23-32 on (s, u')
+      const double f1 = -s + mp.k15 * s * s;
+      const double u2 = s + up * (h.dt * 0.5);
+      const double f2 = -u2 + mp.k15 * u2 * u2;
+      const double u3 = u2 + f1 * mp.dt2_4;
+      const double f3 = -u3 + mp.k15 * u3 * u3;
+      const double v = s + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
+      if (!(fabs(v) >= mp.kappa * (s + fabs(up) * h.dt))) return false;  // cancelling step (or NaN)
+      // E of the new point: cos dt x + sin dt y over rho, with x = sg E_prev, y = sig-turned E_prev
+      const double a = sg * mp.co1, b = sig * mp.si1;
+      const double na = a * ea - b * eb, nb = a * eb + b * ea;
+      sig *= sg;
+      const double iv = mp.rho / v;
+      const v3 p = V(c.x + (na * iv) * X.x + (nb * iv) * Y.x, c.y + (na * iv) * X.y + (nb * iv) * Y.y,
+                     c.z + (na * iv) * X.z + (nb * iv) * Y.z);
+      const double r = fabs(iv);
+      if (!seg_clear_of_box(pp, p, mp.lo, mp.hi, mp.eta * (fmax(rp, r) + mp.scale))) return false;
+      pp = p; rp = r; vprev = v; ea = na; eb = nb;
+    }
+  }
+  return true;
+}
+// Is the camera ray (o, d) a proven miss?  Schwarzschild builds only; the reference-work
+// counting passes (COUNT without count_exec) always march exactly.
+template <bool COUNT>
+__device__ __noinline__ bool camera_miss_proof_call(const KParams& kp, v3 o, v3 d, Counters& cn) {
+  return camera_miss_proof<COUNT>(kp, o, d, cn);
+}
+// NI: out of line (the register-heavy per-pixel-loop builds keep their occupancy)
+template <bool COUNT, bool KERR, bool NI = false>
+__device__ __forceinline__ bool camera_proven_miss(const KParams& kp, v3 o, v3 d, Counters& cn) {
+  if (KERR || !kp.miss.on || (COUNT && !kp.count_exec)) return false;
+  RRT_T0(tp0);
+  const bool r = NI ? camera_miss_proof_call<COUNT>(kp, o, d, cn) : camera_miss_proof<COUNT>(kp, o, d, cn);
+  RRT_ACC(t_proof, tp0);
+  return r;
 }
 
 // query() behind a call: the caller keeps only what is live across the call, the walk gets the

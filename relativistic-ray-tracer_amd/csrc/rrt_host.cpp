@@ -943,6 +943,31 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     kp.hole.r_esc2 = e2 > f2 ? e2 : f2;
     kp.hole.kerr_max_steps = 4 * kp.hole.steps;
   }
+  {  // camera-ray miss proof constants (rrt_device.h camera_miss_proof)
+    const DHole& h = kp.hole;
+    DMissProof& mp = kp.miss;
+    const Box& rb = c->nodes[0].bb;
+    const double rho = std::sqrt(h.cos_dt * h.cos_dt + h.sin_dt * h.sin_dt);
+    mp.rho = rho; mp.inv_rho = 1.0 / rho;
+    mp.co1 = h.cos_dt / rho; mp.si1 = h.sin_dt / rho; mp.inv_si = 1.0 / h.sin_dt;
+    mp.k15 = 1.5 * h.r;
+    mp.dt2_4 = h.dt * h.dt / 4.0; mp.dt2_6 = h.dt * h.dt / 6.0;
+    mp.kappa = 1e-3;
+    mp.eta = 1e-5;
+    const double lo[3] = {rb.mn.x, rb.mn.y, rb.mn.z}, hi[3] = {rb.mx.x, rb.mx.y, rb.mx.z};
+    double sc = 1.0;
+    for (int k = 0; k < 3; ++k) {
+      mp.lo[k] = lo[k]; mp.hi[k] = hi[k];
+      sc = std::max(sc, std::max(std::fabs(lo[k] - h.c[k]), std::fabs(hi[k] - h.c[k])));
+    }
+    mp.scale = 2.0 * sc;
+    bool fin = std::isfinite(mp.scale) && std::isfinite(h.r) && h.r >= 0.0;
+    for (int k = 0; k < 3; ++k) fin = fin && std::isfinite(h.c[k]);
+    // the recurrence needs a proper turn per step (0 < dt < pi, sin dt > 0)
+    mp.on = (h.kind == RRT_METRIC_SCHWARZSCHILD && fin && h.dt > 0.0 && h.dt < 3.0 && h.sin_dt > 0.0 &&
+             h.steps >= 1 && !(p->flags & RRT_RENDER_NO_MISS_PROOF))
+                ? 1u : 0u;
+  }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
   kp.direct_hemisphere = p->direct_hemisphere; kp.seed = p->seed;

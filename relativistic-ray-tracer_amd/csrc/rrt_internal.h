@@ -97,6 +97,20 @@ struct DGrid {
   int32_t pad;
 };
 
+// Camera-ray miss proof (rrt_device.h camera_miss_proof): the constants of the
+// planar recurrence that the reference's Schwarzschild march follows, and the margins.
+struct DMissProof {
+  double co1, si1;        // cos_dt / rho, sin_dt / rho  (rho = |(cos_dt, sin_dt)|)
+  double rho, inv_rho, inv_si;
+  double k15;             // 1.5 * r_s: f(u) = -u + k15 u^2 (blackhole.cpp:13-15)
+  double dt2_4, dt2_6;    // dt^2 / 4, dt^2 / 6
+  double kappa;           // a step whose |v| < kappa (|s| + |up dt|) is not certain: no proof
+  double eta;             // relative position margin (>= 1e3 x the measured deviation bound)
+  double scale;           // scene distance scale about the hole (margin floor)
+  double lo[3], hi[3];    // root box
+  uint32_t on, pad;
+};
+
 #define RRT_MAX_QUEUES 8
 #define RRT_QUEUE_STRIDE 16  // counters 64 B apart
 
@@ -122,6 +136,7 @@ struct KParams {
   uint32_t n_big;
   DCamera cam;
   DHole hole;
+  DMissProof miss;
   DEnv env;
   // render
   uint32_t ns_aa, max_ray_depth, ns_area_light, samples_per_batch;

@@ -118,7 +118,8 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
 template <bool DEEP, bool COUNT, int LEAN>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
-  if (!trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
+  if (camera_proven_miss<COUNT, LEAN == V_KERR, LEAN == 0>(kp, o, d, cn) ||
+      !trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
     return (!is_lean(LEAN) && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;

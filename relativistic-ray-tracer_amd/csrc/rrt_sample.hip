@@ -109,16 +109,27 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 }  // namespace rrt
 
 #if RRT_PROFILE
-__device__ unsigned long long rrt_prof[8];
+// [0..7] per-phase wave cycles (busiest lane per wave, summed): total, camera queries, micro
+// steps, camera walks, miss proofs, shadow queries, shadow walks, -; [8] min start, [9] max end,
+// [10] waves, [11] first exhaustion (wall clock); then per-wave end / start / work records
+#define RRT_PROF_HDR 16
+__device__ unsigned long long rrt_prof[RRT_PROF_HDR];
 __device__ unsigned long long rrt_prof_ends[16384], rrt_prof_starts[16384], rrt_prof_work[16384];
-extern "C" int rrt_prof_read(unsigned long long* out) {  // out: 8 + 3 * 16384
+// slowest pixels: bucket (pixel slot % 64) keeps max(elapsed wall ticks << 24 | slot)
+__device__ unsigned long long rrt_prof_slow[64];
+extern "C" int rrt_prof_read_slow(unsigned long long* out) {  // out: 64; resets
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof_slow), sizeof(rrt_prof_slow)) != hipSuccess) return -1;
+  unsigned long long z[64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rrt_prof_slow), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+extern "C" int rrt_prof_read(unsigned long long* out) {  // out: RRT_PROF_HDR + 3 * 16384
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof), sizeof(rrt_prof)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(rrt_prof_ends), sizeof(rrt_prof_ends)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out + 8 + 16384, HIP_SYMBOL(rrt_prof_starts), sizeof(rrt_prof_starts)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out + RRT_PROF_HDR, HIP_SYMBOL(rrt_prof_ends), sizeof(rrt_prof_ends)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + RRT_PROF_HDR + 16384, HIP_SYMBOL(rrt_prof_starts), sizeof(rrt_prof_starts)) != hipSuccess)
     return -1;
-  if (hipMemcpyFromSymbol(out + 8 + 2 * 16384, HIP_SYMBOL(rrt_prof_work), sizeof(rrt_prof_work)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out + RRT_PROF_HDR + 2 * 16384, HIP_SYMBOL(rrt_prof_work), sizeof(rrt_prof_work)) != hipSuccess)
     return -1;
-  unsigned long long z[8] = {0, 0, 0, 0, ~0ull, 0, 0, ~0ull};
+  unsigned long long z[RRT_PROF_HDR] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, ~0ull};
   return hipMemcpyToSymbol(HIP_SYMBOL(rrt_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
@@ -161,7 +172,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         if (b >= kp.n_blocks) {
           pool_empty = true;
 #if RRT_PROFILE
-          if (lane == 0) atomicMin(&rrt_prof[3 + 4], (unsigned long long)wall_clock64());  // first exhaustion
+          if (lane == 0) atomicMin(&rrt_prof[11], (unsigned long long)wall_clock64());  // first exhaustion
 #endif
           break;
         }
@@ -212,7 +223,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
     spec s = S(0, 0, 0);
     {
       Isect is;
-      if (query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn)) {  // est_radiance (:103-123)
+      const v3 wd = unit(w);
+      if (!camera_proven_miss<COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
+          query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
         else if (is_lean(LEAN)) s = e + direct_importance_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
@@ -252,8 +265,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 #if RRT_PROFILE
   // wave time per phase ~ the busiest lane's; summed over waves (tools/phase_profile.py)
   const uint64_t t_end = clock64(), w_end = wall_clock64();
-  uint64_t v[4] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav};
-  for (int k = 0; k < 4; ++k) {
+  uint64_t v[8] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0};
+  for (int k = 0; k < 8; ++k) {
     for (int off = 32; off > 0; off >>= 1) {
       const uint64_t o2 = __shfl_xor(v[k], off);
       v[k] = v[k] > o2 ? v[k] : o2;
@@ -263,9 +276,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
   uint32_t ns = prof_samples;
   for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off);
   if (lane == 0) {  // [4] min start, [5] max end, [6] waves, [7] first exhaustion; per-wave records
-    atomicMin(&rrt_prof[4], (unsigned long long)w_start);
-    atomicMax(&rrt_prof[5], (unsigned long long)w_end);
-    const unsigned long long w = atomicAdd(&rrt_prof[6], 1ull) & 16383;
+    atomicMin(&rrt_prof[8], (unsigned long long)w_start);
+    atomicMax(&rrt_prof[9], (unsigned long long)w_end);
+    const unsigned long long w = atomicAdd(&rrt_prof[10], 1ull) & 16383;
     rrt_prof_ends[w] = w_end;
     rrt_prof_starts[w] = w_start;
     rrt_prof_work[w] = ((unsigned long long)prof_blocks << 32) | ns;
@@ -293,6 +306,14 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 #define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
 #endif
 
+#define RRT_SLOTS 64  // draw-offset slots per group and step
+#ifndef RRT_TAIL_PRIO
+#define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
+#endif
+#ifndef RRT_PRIO_TICKS
+#define RRT_PRIO_TICKS 50000  // 0.5 ms of wall clock (100 MHz): a long-running pixel
+#endif
+
 // Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
 // run with only the lane's own few speculation registers live.
 struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
@@ -300,6 +321,9 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   uint32_t px[32], py[32], slot[32], O[32], i[32], hyp[32];
   float rr[32], rg[32], rb[32];
   double s1[32], s2[32];
+  // draw-offset slots of the current step (see the camera-query section): state 0 unknown,
+  // 1 miss, 2 hit; owner = group lane whose ShadeLds slot holds the hit record
+  uint8_t sst[32][RRT_SLOTS], sown[32][RRT_SLOTS];
 };
 
 template <int LEAN, int WAVES>
@@ -328,6 +352,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
+  uint64_t t_claim = 0;  // when the group claimed its pixel (wall clock)
 
   for (;;) {
     // ---- claim a pixel (one atomic per group)
@@ -346,7 +371,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       if (p >= kp.n_pixels) {
         done = true;
 #if RRT_PROFILE
-        if (gl == 0) atomicMin(&rrt_prof[7], (unsigned long long)wall_clock64());
+        if (gl == 0) atomicMin(&rrt_prof[11], (unsigned long long)wall_clock64());
 #endif
       } else {
 #if RRT_PROFILE
@@ -375,47 +400,137 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
             }
           }
           have = true;
+          t_claim = wall_clock64();
         }
       }
     }
     if (__ballot(!done) == 0) break;
+    // Tail latency: a pixel whose rounds are long (the costliest ones -- long walks next to the
+    // hole and the geometry) keeps its wave busy long after the claim queue runs dry.  A wave
+    // whose oldest pixel has been running for a while takes issue priority over the other waves
+    // of its SIMD, so the costliest pixels finish early instead of forming the frame's tail.
+    auto tail_prio = [&]() {
+      if (!RRT_TAIL_PRIO) return;
+      const uint64_t age = have ? wall_clock64() - t_claim : 0;
+      if (__ballot(age > 4 * RRT_PRIO_TICKS)) __builtin_amdgcn_s_setprio(3);
+      else if (__ballot(age > RRT_PRIO_TICKS)) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+    };
+    tail_prio();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---- camera queries at speculated draw offsets, re-run until the offsets are consistent
-    // samples this step: up to the next adaptive check (no sample past a possible stop), at most G
+    // ---- camera queries by draw-offset slot.  Sample k of the step starts at draw offset
+    // O + Dm * m_k, where slot m_0 = 0 and m_{k+1} = m_k + (hit_k ? Dh / Dm : 1): a slot's ray
+    // (its jitter draws) is the same whichever sample lands on it, so slot results are shared.
+    // Round 1 computes the slots of the hypothesis (all samples hit or all miss, as the pixel's
+    // last sample); every round then walks the chain over the known slots and hands the first
+    // unknown slot -- and the ones after it, taking unknowns as misses -- to lanes whose slot is
+    // off the chain.  Each round resolves at least one more sample; all-hit and all-miss
+    // pixels take one round, mixed ones a few.  A chain that leaves the slot window ends the
+    // step early (the next step continues it).
     const int done_i = (int)lget(gs.i, gid);
     const int to_check = (int)kp.samples_per_batch - done_i % (int)kp.samples_per_batch;
     const int left = min((int)kp.ns_aa - done_i, to_check);
-    const bool act = have && (int)gl < left;
-    bool valid = false, hit = false, h = lget(gs.hyp, gid) != 0;
-    uint32_t off = 0;
+    const uint32_t S1 = Dh / Dm;  // slots a hit consumes
+    const uint32_t O0 = lget(gs.O, gid);
+    for (uint32_t m = gl; m < RRT_SLOTS; m += G) lput(&gs.sst[gid][0], m, (uint8_t)0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t my = RRT_SLOTS;  // slot to compute this round (RRT_SLOTS: none)
+    if (have && (int)gl < left) {
+      const uint32_t m0 = gl * (lget(gs.hyp, gid) ? S1 : 1u);
+      if (m0 < RRT_SLOTS) my = m0;
+    }
+    uint32_t held = RRT_SLOTS;  // slot whose hit record this lane's ShadeLds slot holds
+    uint32_t mk = 0;            // slot of this lane's sample (lane gl = sample gl of the step)
+    bool hk = false;
+    int n_step = 0;             // samples the step resolves
     for (;;) {
-      const bool need = act && !valid;
+      const bool need = my < RRT_SLOTS;
       if (__ballot(need) == 0) break;
+      tail_prio();
 #if RRT_PROFILE
       ++prof_samples;
 #endif
-      const uint64_t lt = ((1ull << lane) - 1ull) & ~((1ull << gbase) - 1ull);  // group lanes before me
-      const uint32_t nh = (uint32_t)__popcll(__ballot(act && h) & lt);
       if (need) {
-        off = lget(gs.O, gid) + nh * Dh + (gl - nh) * Dm;
-        Rng g; g.key = lget(gs.key, gid); g.ctr = off;
+        Rng g; g.key = lget(gs.key, gid); g.ctr = O0 + my * Dm;
         double jx, jy; g.grid(jx, jy);
         const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
         const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;  // Camera::generate_ray (:182-187)
         const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
         const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
         Isect is;
-        hit = query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn);
-        if (hit) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
+        const v3 wd = unit(w);
+        const bool h = !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
+                       query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn);
+        if (h) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
+        held = my;
+        lput(&gs.sst[gid][0], my, (uint8_t)(h ? 2 : 1));
+        lput(&gs.sown[gid][0], my, (uint8_t)gl);
       }
-      const uint32_t na = (uint32_t)__popcll(__ballot(act && hit) & lt);
-      valid = act && (lget(gs.O, gid) + na * Dh + (gl - na) * Dm == off);
-      h = hit;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // walk the chain over the known slots (group-uniform)
+      uint32_t m = 0;
+      int k = 0;
+      bool on_chain = false;
+      for (; k < left && m < RRT_SLOTS; ++k) {
+        const uint32_t st = lget(&gs.sst[gid][0], m);
+        if (st == 0) break;
+        on_chain |= m == held;
+        if (k == (int)gl) { mk = m; hk = st == 2; }
+        m += st == 2 ? S1 : 1u;
+      }
+      n_step = k;
+      my = RRT_SLOTS;
+      const bool open = have && k < left && m < RRT_SLOTS;  // unresolved samples remain
+      // lanes off the chain take the unknown slots along the continuation (unknowns as misses)
+      const bool lane_free = open && !on_chain;
+      const uint64_t lt = ((1ull << lane) - 1ull) & ~((1ull << gbase) - 1ull);  // group lanes before me
+      const uint32_t rank = (uint32_t)__popcll(__ballot(lane_free) & lt);
+      if (lane_free) {
+        uint32_t mm = m, j = 0;
+        for (int kk = k; kk < left && mm < RRT_SLOTS; ++kk) {
+          const uint32_t st = lget(&gs.sst[gid][0], mm);
+          if (st == 0) {
+            if (j == rank) { my = mm; break; }
+            ++j;
+          }
+          mm += st == 2 ? S1 : 1u;
+        }
+        // the hit record this lane gives up is no longer available: its slot becomes unknown
+        if (my < RRT_SLOTS && held < RRT_SLOTS && lget(&gs.sst[gid][0], held) == 2)
+          lput(&gs.sst[gid][0], held, (uint8_t)0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const uint64_t hits = __ballot(act && hit);
+    const bool act = have && (int)gl < n_step;
+    const bool hit = act && hk;
+    const uint32_t off = O0 + mk * Dm;
+    {  // move each hit sample's record into its own lane's ShadeLds slot
+      const uint32_t src = (t - gl) + lget(&gs.sown[gid][0], mk);
+      Isect is0 = {};
+      if (hit && src != t) {
+        is0.hit_p = V(lget(cl.hp[0], src), lget(cl.hp[1], src), lget(cl.hp[2], src));
+        is0.n = V(lget(cl.nn[0], src), lget(cl.nn[1], src), lget(cl.nn[2], src));
+        is0.w_out = V(lget(cl.wo[0], src), lget(cl.wo[1], src), lget(cl.wo[2], src));
+        is0.bsdf = (int)lget(cl.bsdf, src);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (hit && src != t) park_hit(cl, t, is0);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint64_t hits = __ballot(hit);
 
     // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
     spec s = S(0, 0, 0);
@@ -444,7 +559,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     // ---- ordered fold by the group leader (raytrace_pixel's loop body, :136-158)
     uint32_t stop = 0;
     if (have && gl == 0) {
-      const int n = left < (int)G ? left : (int)G;
+      const int n = n_step;
       spec ret = S(lget(gs.rr, gid), lget(gs.rg, gid), lget(gs.rb, gid));
       double s1 = lget(gs.s1, gid), s2 = lget(gs.s2, gid);
       int i = (int)lget(gs.i, gid);
@@ -468,6 +583,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       }
       if (stop) {
         const uint32_t slot = lget(gs.slot, gid);
+#if RRT_PROFILE
+        atomicMax(&rrt_prof_slow[slot & 63u], ((wall_clock64() - t_claim) << 24) | (unsigned long long)(slot & 0xffffffu));
+#endif
         const spec r = ret / (float)i;
         kp.rgb[3 * slot] = r.r; kp.rgb[3 * slot + 1] = r.g; kp.rgb[3 * slot + 2] = r.b;
         kp.count[slot] = i;
@@ -483,8 +601,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   }
 #if RRT_PROFILE
   const uint64_t t_end = clock64(), w_end = wall_clock64();
-  uint64_t v[4] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav};
-  for (int k = 0; k < 4; ++k) {
+  uint64_t v[8] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0};
+  for (int k = 0; k < 8; ++k) {
     for (int off2 = 32; off2 > 0; off2 >>= 1) {
       const uint64_t o2 = __shfl_xor(v[k], off2);
       v[k] = v[k] > o2 ? v[k] : o2;
@@ -494,9 +612,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   uint32_t nb = gl == 0 ? prof_blocks : 0;
   for (int off2 = 32; off2 > 0; off2 >>= 1) nb += __shfl_xor(nb, off2);
   if (lane == 0) {
-    atomicMin(&rrt_prof[4], (unsigned long long)w_start);
-    atomicMax(&rrt_prof[5], (unsigned long long)w_end);
-    const unsigned long long w = atomicAdd(&rrt_prof[6], 1ull) & 16383;
+    atomicMin(&rrt_prof[8], (unsigned long long)w_start);
+    atomicMax(&rrt_prof[9], (unsigned long long)w_end);
+    const unsigned long long w = atomicAdd(&rrt_prof[10], 1ull) & 16383;
     rrt_prof_ends[w] = w_end;
     rrt_prof_starts[w] = w_start;
     rrt_prof_work[w] = ((unsigned long long)nb << 32) | prof_samples;
@@ -528,7 +646,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_first_kernel(const KParams* __
     const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     Isect is;
-    const bool hit = query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), unit(w), &is, cn);
+    const v3 wd = unit(w);
+    const bool hit = !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
+                     query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (!hit && !is_lean(LEAN) && kp.env.w) s = env_dir(kp.env, unit(w));
     if (hit) {

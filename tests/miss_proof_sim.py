@@ -1,0 +1,113 @@
+"""numpy mirror of the camera-ray miss proof (relativistic-ray-tracer_amd/csrc/rrt_device.h
+camera_miss_proof), vectorised over rays, with the per-point trace the deviation checks need.
+
+TEST INFRASTRUCTURE ONLY (tests/test_miss_proof.py): the product runs the HIP version.
+
+The proof replaces the reference's march (blackhole.cpp:17-40, bvh.cpp:103-113) for a camera ray
+by the planar recurrence it follows in exact arithmetic and accepts "miss" only when every
+segment of the recurrence clears the root box by a margin far above the recurrence's deviation
+from the reference's floating-point march.  Constants as rrt_host.cpp launch() sets them.
+"""
+import numpy as np
+
+KAPPA = 1e-3
+ETA = 1e-5
+
+
+def constants(bh, lo, hi):
+    c = np.array(bh[:3], np.float64)
+    r, dt = float(bh[3]), float(bh[4])
+    co, si = np.cos(dt), np.sin(dt)
+    rho = np.sqrt(co * co + si * si)
+    sc = max(1.0, float(np.max(np.maximum(np.abs(lo - c), np.abs(hi - c)))))
+    steps = 0
+    while steps * dt < 2 * np.pi:
+        steps += 1
+    return dict(c=c, r=r, dt=dt, co=co, si=si, rho=rho, co1=co / rho, si1=si / rho, k15=1.5 * r,
+                scale=2.0 * sc, lo=lo, hi=hi, steps=steps)
+
+
+def _step0(K, o, d):
+    """The reference's first step from the camera ray (next_micro_ray with max_t = 0)."""
+    c, dt, r = K["c"], K["dt"], K["r"]
+    x = o - c
+    dist = np.sqrt(x[:, 0] * x[:, 0] + x[:, 1] * x[:, 1] + x[:, 2] * x[:, 2])
+    u = 1.0 / dist
+    x = x * u[:, None]
+    dx = (d * x).sum(1)
+    y = d - dx[:, None] * x
+    dy = np.sqrt((y * y).sum(1))
+    y = y * (1.0 / dy)[:, None]
+    up = -u * dx / dy
+    k = 3.0 * r
+    f1 = -u + k * u * u / 2.0
+    u2 = u + up * dt / 2.0
+    f2 = -u2 + k * u2 * u2 / 2.0
+    u3 = u + up * dt / 2.0 + f1 * dt * dt / 4.0
+    f3 = -u3 + k * u3 * u3 / 2.0
+    v = u + (up * dt + (f1 + f2 + f3) * dt * dt / 6.0)
+    p1 = c + (1.0 / v * K["co"])[:, None] * x + (1.0 / v * K["si"])[:, None] * y
+    return x, y, u, up, v, p1
+
+
+def seg_clear(a, b, lo, hi, m):
+    """seg_clear_of_box: the segments a->b miss the box widened by m (per ray)."""
+    l = lo[None, :] - m[:, None]
+    h = hi[None, :] + m[:, None]
+    out = (np.maximum(a, b) < l).any(1) | (np.minimum(a, b) > h).any(1)
+    D = b - a
+    tmin = np.zeros(len(a))
+    tmax = np.ones(len(a))
+    with np.errstate(all="ignore"):
+        for k in range(3):
+            nz = D[:, k] != 0.0
+            i = 1.0 / D[:, k]
+            t0 = (l[:, k] - a[:, k]) * i
+            t1 = (h[:, k] - a[:, k]) * i
+            tmin = np.where(nz, np.fmax(tmin, np.fmin(t0, t1)), tmin)
+            tmax = np.where(nz, np.fmin(tmax, np.fmax(t0, t1)), tmax)
+    return out | (tmin > tmax + 1e-9)
+
+
+def run(K, o, d, step0_clear):
+    """The proof for rays (o, d).  step0_clear[i]: the reference's root test fails on segment 0.
+    Returns (proven [n], points [steps+1, n, 3] of the recurrence (NaN once a ray bails),
+    margins [steps+1, n])."""
+    n = len(o)
+    steps = K["steps"]
+    X, Y, s, up, vprev, p1 = _step0(K, o, d)
+    pts = np.full((steps + 1, n, 3), np.nan)
+    mrg = np.full((steps + 1, n), np.nan)
+    pts[0], pts[1] = o, p1
+    alive = step0_clear.copy()
+    ea = np.full(n, K["co1"])
+    eb = np.full(n, K["si1"])
+    sig = np.ones(n)
+    pp = p1
+    rp = np.sqrt(((p1 - K["c"]) ** 2).sum(1))
+    with np.errstate(all="ignore"):
+        for j in range(1, steps):
+            sg = np.where(vprev < 0.0, -1.0, 1.0)
+            up = (vprev * K["co1"] - K["rho"] * s) / K["si"]
+            s = np.abs(vprev) / K["rho"]
+            f1 = -s + K["k15"] * s * s
+            u2 = s + up * (K["dt"] * 0.5)
+            f2 = -u2 + K["k15"] * u2 * u2
+            u3 = u2 + f1 * (K["dt"] * K["dt"] / 4.0)
+            f3 = -u3 + K["k15"] * u3 * u3
+            v = s + up * K["dt"] + (f1 + f2 + f3) * (K["dt"] * K["dt"] / 6.0)
+            alive &= np.abs(v) >= KAPPA * (s + np.abs(up) * K["dt"])
+            a = sg * K["co1"]
+            b = sig * K["si1"]
+            na = a * ea - b * eb
+            nb = a * eb + b * ea
+            sig = sig * sg
+            iv = K["rho"] / v
+            p = K["c"] + (na * iv)[:, None] * X + (nb * iv)[:, None] * Y
+            r = np.abs(iv)
+            m = ETA * (np.maximum(rp, r) + K["scale"])
+            alive &= seg_clear(pp, p, K["lo"], K["hi"], m)
+            pts[j + 1] = np.where(alive[:, None], p, np.nan)
+            mrg[j + 1] = np.where(alive, m, np.nan)
+            pp, rp, vprev, ea, eb = p, r, v, na, nb
+    return alive, pts, mrg

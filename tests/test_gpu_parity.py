@@ -53,10 +53,11 @@ def check(c, rgb, cnt, draws):
 # every kernel path must meet the same bar: default (sample-parallel kernel, clean-tree BVH walk,
 # empty-space grid), the reference-tree walk without the grid, the lane-per-pixel per-sample
 # kernel, the per-pixel-loop kernel and the wavefront state-machine kernel; the sample-parallel
-# kernel also with one chip-wide claim queue, one queue per XCD, and in list order
+# kernel also with one chip-wide claim queue, one queue per XCD, and in list order; and the
+# default path with every camera ray marched exactly (no miss proof)
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "xcdqueues": rrt.RRT_RENDER_XCD_QUEUES,
-            "ordered": rrt.RRT_RENDER_ORDERED,
+            "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "wavefront": rrt.RRT_RENDER_WAVEFRONT}
 
@@ -72,11 +73,13 @@ def test_small_cases(gpu, name, variant):
     check(c, rgb, cnt, draws)
 
 
+@pytest.mark.parametrize("proof", [True, False])
 @pytest.mark.parametrize("name", ["cfg1_spheres_480x360_s8", "cfg2_spheres_1080p_s64_flat", "cfg3_bunny_1080p_s64"])
-def test_baseline_frames(gpu, name):
-    """The BASELINE.json configs, full frames, bit-exact against the reference."""
+def test_baseline_frames(gpu, name, proof):
+    """The BASELINE.json configs, full frames, bit-exact against the reference (with the
+    camera-ray miss proof, the default, and with every camera ray marched exactly)."""
     c = Case(name)
-    rgb, cnt, draws, _ = render(gpu, c)
+    rgb, cnt, draws, _ = render(gpu, c, flags=0 if proof else rrt.RRT_RENDER_NO_MISS_PROOF)
     check(c, rgb, cnt, draws)
 
 

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase wave time of the depth<=1 per-sample kernel, from a build with
+"""Diagnostic: per-phase wave time of the depth<=1 sample-parallel (batch) kernel, from a build with
 -DRRT_PROFILE=1 (make -C relativistic-ray-tracer_amd EXTRA=-DRRT_PROFILE=1), loaded through
-RRT_LIB.  Prints the share of wave time spent in the geodesic queries, their micro steps and
-their BVH walks (busiest lane per wave, summed over waves)."""
+RRT_LIB.  Prints the share of wave time spent in camera queries, miss proofs, shadow queries, their micro
+steps and BVH walks (busiest lane per wave, summed over waves)."""
 import argparse
 import ctypes as C
 import json
@@ -22,44 +22,64 @@ from golden_cases import Case  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="cfg3_bunny_1080p_s64")
-    ap.add_argument("--flags", type=int, nargs="+", default=[0, rrt.RRT_RENDER_NO_CLEAN])
+    ap.add_argument("--flags", type=int, nargs="+", default=[0, rrt.RRT_RENDER_NO_MISS_PROOF])
+    ap.add_argument("--tiles", type=int, nargs="*", default=None, help="x y pairs of 32x32 tiles (default: all)")
+    ap.add_argument("--region", type=int, nargs=4, default=None, help="x0 y0 w h: render only this region")
     a = ap.parse_args()
     c = Case(a.case)
     g = c.cfg
     L = rrt.lib()
     L.rrt_prof_read.argtypes = [C.c_void_p]
+    L.rrt_prof_read_slow.argtypes = [C.c_void_p]
     r = rrt.Renderer(0)
     r.set_scene(rrt.SceneFile(c.scene_path))
     r.set_camera(rrt.load_camera(c.camera_path))
     r.set_black_hole(g["bh"][:3], g["bh"][3], g["bh"][4])
     tiles = rrt.partition_tiles(c.frame_w, c.frame_h, 32, 0, 1)
+    if a.tiles:
+        tiles = np.array(a.tiles, np.uint32).reshape(-1, 2)
     n = len(tiles) * 1024
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
-    buf = np.zeros(8 + 3 * 16384, np.uint64)
+    HDR = 16
+    buf = np.zeros(HDR + 3 * 16384, np.uint64)
     out = {}
     for fl in a.flags:
         p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
                               ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
                               max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=fl)
         L.rrt_prof_read(buf.ctypes.data)
-        r.render_tiles_device(p, tiles, 32, prgb.data_ptr(), pcnt.data_ptr())
+        L.rrt_prof_read_slow(np.zeros(64, np.uint64).ctypes.data)
+        if a.region:
+            r.render(p, *a.region)
+        else:
+            r.render_tiles_device(p, tiles, 32, prgb.data_ptr(), pcnt.data_ptr())
         ms = r.stats().last_kernel_ms
         L.rrt_prof_read(buf.ctypes.data)
-        tot, tq, tm, tt = (float(v) for v in buf[:4])
-        t0, t1, nw, tex = int(buf[4]), int(buf[5]), int(buf[6]), int(buf[7])
+        tot, tq, tm, tt, tp, tsq, tst = (float(v) for v in buf[:7])
+        t0, t1, nw, tex = int(buf[8]), int(buf[9]), int(buf[10]), int(buf[11])
         span = t1 - t0
         m = min(nw, 16384)
-        ends = (buf[8:8 + m].astype(np.float64) - t0) / span
-        starts = (buf[8 + 16384:8 + 16384 + m].astype(np.float64) - t0) / span
-        work = buf[8 + 2 * 16384:8 + 2 * 16384 + m]
+        ends = (buf[HDR:HDR + m].astype(np.float64) - t0) / span
+        starts = (buf[HDR + 16384:HDR + 16384 + m].astype(np.float64) - t0) / span
+        work = buf[HDR + 2 * 16384:HDR + 2 * 16384 + m]
         blocks, samples = (work >> np.uint64(32)).astype(np.int64), (work & np.uint64(0xffffffff)).astype(np.int64)
         res = blocks > 0
         np.savez(f"gpurun_out/waves_{fl}.npz", ends=ends, starts=starts, blocks=blocks, samples=samples)
+        slow = np.zeros(64, np.uint64)
+        L.rrt_prof_read_slow(slow.ctypes.data)
+        slow_px = []
+        for v in sorted((int(x) for x in slow if x), reverse=True)[:16]:
+            sl, ticks = v & 0xffffff, v >> 24
+            t_i, rr = sl // 1024, sl % 1024
+            slow_px.append({"x": int(tiles[t_i][0]) + rr % 32, "y": int(tiles[t_i][1]) + rr // 32,
+                            "ms": ticks / (span / ms)})
         out[fl] = {"kernel_ms": ms, "ticks_per_ms": span / ms, "waves": nw, "waves_with_work": int(res.sum()),
                    "exhausted_at": (tex - t0) / span, "wave_cycles": tot,
-                   "query": tq / tot, "micro": tm / tot, "walk": tt / tot,
-                   "other_in_query": (tq - tm - tt) / tot, "outside_query": 1 - tq / tot,
+                   "camera_query": tq / tot, "micro_all": tm / tot, "camera_walk": tt / tot,
+                   "miss_proof": tp / tot, "shadow_query": tsq / tot, "shadow_walk": tst / tot,
+                   "outside_queries_and_proof": 1 - (tq + tp + tsq) / tot,
+                   "slowest_pixels": slow_px,
                    "busy_frac_working_waves": float(((ends - starts)[res]).sum() / max(res.sum(), 1)),
                    "working_wave_end_q": [round(float(q), 3) for q in np.quantile(ends[res], [0.05, 0.25, 0.5, 0.75, 0.95, 1.0])],
                    "working_wave_start_q": [round(float(q), 3) for q in np.quantile(starts[res], [0.05, 0.5, 0.95, 1.0])],
