@@ -848,8 +848,8 @@ __device__ __forceinline__ bool camera_miss_proof(const KParams& kp, v3 o, v3 d,
     const v3 X = m0.x, Y = m0.y;
     double s = m0.u, up = m0.up, vprev = m0.v;
     double ea = mp.co1, eb = mp.si1, sig = 1.0;  // E of the point just placed, in (X, Y); sense of y from x
-    v3 pp = e;
-    double rp = sqrt(norm2(e - c));
+    double rp = mp.rho / fabs(vprev);             // its distance from the hole
+    const double si2 = h.sin_dt * h.sin_dt;
     for (int j = 1; j < h.steps; ++j) {
       // the next step's start: s, u', and its frame (x = sg E, y = E turned by sig)
       const double sg = vprev < 0.0 ? -1.0 : 1.0;
@@ -867,12 +867,24 @@ __device__ __forceinline__ bool camera_miss_proof(const KParams& kp, v3 o, v3 d,
       const double a = sg * mp.co1, b = sig * mp.si1;
       const double na = a * ea - b * eb, nb = a * eb + b * ea;
       sig *= sg;
-      const double iv = mp.rho / v;
-      const v3 p = V(c.x + (na * iv) * X.x + (nb * iv) * Y.x, c.y + (na * iv) * X.y + (nb * iv) * Y.y,
-                     c.z + (na * iv) * X.z + (nb * iv) * Y.z);
-      const double r = fabs(iv);
-      if (!seg_clear_of_box(pp, p, mp.lo, mp.hi, mp.eta * (fmax(rp, r) + mp.scale))) return false;
-      pp = p; rp = r; vprev = v; ea = na; eb = nb;
+      // The segment A -> B, A = rho E_prev / vprev, B = rho E / v about the hole, with
+      // E_prev . E = sg co1 and |E_prev x E| = si1: its distance from the hole from scalars alone
+      // (foot of the perpendicular inside: line distance^2 = sin^2 dt / D, else the nearer end).
+      const double av = fabs(v), avp = fabs(vprev);
+      const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);  // |B| (upper bound)
+      const double rb = mp.r_ball + mp.eta * (fmax(rp, r) + mp.scale);
+      const double D = v * v + vprev * vprev - 2.0 * mp.co1 * avp * v;
+      const bool inside = v * (mp.co1 * avp - v) < 0.0 && avp * (avp - mp.co1 * v) > 0.0;
+      const bool far = inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(v * v, vprev * vprev);
+      if (!far) {  // within reach of the root box: the segment itself against the widened box
+        const double ia = mp.rho / vprev, ib = mp.rho / v;
+        const v3 pa = V(c.x + (ea * ia) * X.x + (eb * ia) * Y.x, c.y + (ea * ia) * X.y + (eb * ia) * Y.y,
+                        c.z + (ea * ia) * X.z + (eb * ia) * Y.z);
+        const v3 pb = V(c.x + (na * ib) * X.x + (nb * ib) * Y.x, c.y + (na * ib) * X.y + (nb * ib) * Y.y,
+                        c.z + (na * ib) * X.z + (nb * ib) * Y.z);
+        if (!seg_clear_of_box(pa, pb, mp.lo, mp.hi, mp.eta * (fmax(rp, r) + mp.scale))) return false;
+      }
+      rp = r; vprev = v; ea = na; eb = nb;
     }
   }
   return true;

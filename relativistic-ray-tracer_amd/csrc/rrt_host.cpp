@@ -961,6 +961,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       sc = std::max(sc, std::max(std::fabs(lo[k] - h.c[k]), std::fabs(hi[k] - h.c[k])));
     }
     mp.scale = 2.0 * sc;
+    double rb2 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double e = std::max(std::fabs(lo[k] - h.c[k]), std::fabs(hi[k] - h.c[k]));
+      rb2 += e * e;
+    }
+    mp.r_ball = std::sqrt(rb2) * (1.0 + 1e-9);
     bool fin = std::isfinite(mp.scale) && std::isfinite(h.r) && h.r >= 0.0;
     for (int k = 0; k < 3; ++k) fin = fin && std::isfinite(h.c[k]);
     // the recurrence needs a proper turn per step (0 < dt < pi, sin dt > 0)

@@ -108,6 +108,7 @@ struct DMissProof {
   double eta;             // relative position margin (>= 1e3 x the measured deviation bound)
   double scale;           // scene distance scale about the hole (margin floor)
   double lo[3], hi[3];    // root box
+  double r_ball;          // distance from the hole to the farthest root-box corner (x (1 + 1e-9))
   uint32_t on, pad;
 };
 

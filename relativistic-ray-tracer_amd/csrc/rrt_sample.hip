@@ -322,7 +322,8 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   float rr[32], rg[32], rb[32];
   double s1[32], s2[32];
   // draw-offset slots of the current step (see the camera-query section): state 0 unknown,
-  // 1 miss, 2 hit; owner = group lane whose ShadeLds slot holds the hit record
+  // 1 miss, 2 hit, 3 hit whose record was given up; owner = group lane whose ShadeLds slot holds
+  // the hit record
   uint8_t sst[32][RRT_SLOTS], sown[32][RRT_SLOTS];
 };
 
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 #if RRT_PROFILE
   const uint64_t t_start = clock64(), w_start = wall_clock64();
   uint32_t prof_blocks = 0, prof_samples = 0;  // pixels claimed, query rounds
+  uint32_t px_rounds = 0, px_steps = 0;           // of the group's current pixel
 #endif
 
   bool have = false, done = false;
@@ -401,6 +403,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
           }
           have = true;
           t_claim = wall_clock64();
+#if RRT_PROFILE
+          px_rounds = 0; px_steps = 0;
+#endif
         }
       }
     }
@@ -426,10 +431,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     // (its jitter draws) is the same whichever sample lands on it, so slot results are shared.
     // Round 1 computes the slots of the hypothesis (all samples hit or all miss, as the pixel's
     // last sample); every round then walks the chain over the known slots and hands the first
-    // unknown slot -- and the ones after it, taking unknowns as misses -- to lanes whose slot is
-    // off the chain.  Each round resolves at least one more sample; all-hit and all-miss
-    // pixels take one round, mixed ones a few.  A chain that leaves the slot window ends the
-    // step early (the next step continues it).
+    // unknown slot -- and the unknown ones after it -- to lanes whose slot is off the chain.
+    // Each round resolves at least one more sample; all-hit and all-miss pixels take one round,
+    // mixed ones two or three.  A chain that leaves the slot window ends the step early (the
+    // next step continues it).
     const int done_i = (int)lget(gs.i, gid);
     const int to_check = (int)kp.samples_per_batch - done_i % (int)kp.samples_per_batch;
     const int left = min((int)kp.ns_aa - done_i, to_check);
@@ -444,6 +449,20 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const uint32_t m0 = gl * (lget(gs.hyp, gid) ? S1 : 1u);
       if (m0 < RRT_SLOTS) my = m0;
     }
+    // the camera query of slot sl (Camera::generate_ray, part1_code.cpp:182-187, at its jitter)
+    auto slot_query = [&](uint32_t sl, Isect* is) -> bool {
+      Rng g; g.key = lget(gs.key, gid); g.ctr = O0 + sl * Dm;
+      double jx, jy; g.grid(jx, jy);
+      const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
+      const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
+      const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+      const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+      const v3 wd = unit(w);
+      return !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
+             query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, is, cn);
+    };
+    const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;  // this group's lanes
+    const uint64_t lt = ((1ull << lane) - 1ull) & gmask;                         // group lanes before me
     uint32_t held = RRT_SLOTS;  // slot whose hit record this lane's ShadeLds slot holds
     uint32_t mk = 0;            // slot of this lane's sample (lane gl = sample gl of the step)
     bool hk = false;
@@ -454,18 +473,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       tail_prio();
 #if RRT_PROFILE
       ++prof_samples;
+      ++px_rounds;
 #endif
       if (need) {
-        Rng g; g.key = lget(gs.key, gid); g.ctr = O0 + my * Dm;
-        double jx, jy; g.grid(jx, jy);
-        const double sx = (double)lget(gs.px, gid) + jx, sy = (double)lget(gs.py, gid) + jy;
-        const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;  // Camera::generate_ray (:182-187)
-        const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
-        const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
         Isect is;
-        const v3 wd = unit(w);
-        const bool h = !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
-                       query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn);
+        const bool h = slot_query(my, &is);
         if (h) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
         held = my;
         lput(&gs.sst[gid][0], my, (uint8_t)(h ? 2 : 1));
@@ -476,23 +488,31 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // walk the chain over the known slots (group-uniform)
       uint32_t m = 0;
-      int k = 0;
+      int k = 0, kh = 0;
       bool on_chain = false;
       for (; k < left && m < RRT_SLOTS; ++k) {
         const uint32_t st = lget(&gs.sst[gid][0], m);
         if (st == 0) break;
         on_chain |= m == held;
-        if (k == (int)gl) { mk = m; hk = st == 2; }
-        m += st == 2 ? S1 : 1u;
+        if (k == (int)gl) { mk = m; hk = st >= 2; }
+        kh += st >= 2;
+        m += st >= 2 ? S1 : 1u;
       }
       n_step = k;
       my = RRT_SLOTS;
       const bool open = have && k < left && m < RRT_SLOTS;  // unresolved samples remain
-      // lanes off the chain take the unknown slots along the continuation (unknowns as misses)
-      const bool lane_free = open && !on_chain;
-      const uint64_t lt = ((1ull << lane) - 1ull) & ~((1ull << gbase) - 1ull);  // group lanes before me
-      const uint32_t rank = (uint32_t)__popcll(__ballot(lane_free) & lt);
-      if (lane_free) {
+      // Lanes off the chain take the unknown slots along the continuation (an unknown slot taken
+      // as the majority outcome of the resolved samples, the pixel's hypothesis before any):
+      // first lanes whose slot needs no record (none, a miss, or a slot the chain has passed),
+      // then lanes holding a hit beyond the frontier, whose outcome stays known (state 3) while
+      // its record is given up (recomputed if the chain lands on it).
+      const uint32_t sth = held < RRT_SLOTS ? lget(&gs.sst[gid][0], held) : 0u;
+      const bool free_a = open && !on_chain && (held >= RRT_SLOTS || held < m || sth != 2);
+      const bool free_b = open && !on_chain && !free_a;
+      const uint64_t ba = __ballot(free_a), bb = __ballot(free_b);
+      const uint32_t rank = free_a ? (uint32_t)__popcll(ba & lt) : (uint32_t)(__popcll(ba & gmask) + __popcll(bb & lt));
+      if (free_a || free_b) {
+        const uint32_t guess = (k > 0 ? 2 * kh >= k : lget(gs.hyp, gid) != 0) ? S1 : 1u;
         uint32_t mm = m, j = 0;
         for (int kk = k; kk < left && mm < RRT_SLOTS; ++kk) {
           const uint32_t st = lget(&gs.sst[gid][0], mm);
@@ -500,11 +520,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
             if (j == rank) { my = mm; break; }
             ++j;
           }
-          mm += st == 2 ? S1 : 1u;
+          mm += st == 0 ? guess : st >= 2 ? S1 : 1u;
         }
-        // the hit record this lane gives up is no longer available: its slot becomes unknown
-        if (my < RRT_SLOTS && held < RRT_SLOTS && lget(&gs.sst[gid][0], held) == 2)
-          lput(&gs.sst[gid][0], held, (uint8_t)0);
+        if (my < RRT_SLOTS && free_b) lput(&gs.sst[gid][0], held, (uint8_t)3);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -513,10 +531,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     const bool act = have && (int)gl < n_step;
     const bool hit = act && hk;
     const uint32_t off = O0 + mk * Dm;
-    {  // move each hit sample's record into its own lane's ShadeLds slot
+    {  // move each hit sample's record into its own lane's ShadeLds slot (recompute a given-up one)
+      const bool lost = hit && lget(&gs.sst[gid][0], mk) == 3;
       const uint32_t src = (t - gl) + lget(&gs.sown[gid][0], mk);
+      const bool move = hit && !lost && src != t;
       Isect is0 = {};
-      if (hit && src != t) {
+      if (move) {
         is0.hit_p = V(lget(cl.hp[0], src), lget(cl.hp[1], src), lget(cl.hp[2], src));
         is0.n = V(lget(cl.nn[0], src), lget(cl.nn[1], src), lget(cl.nn[2], src));
         is0.w_out = V(lget(cl.wo[0], src), lget(cl.wo[1], src), lget(cl.wo[2], src));
@@ -525,7 +545,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (hit && src != t) park_hit(cl, t, is0);
+      if (lost) slot_query(mk, &is0);  // the same ray: the same hit
+      if (move || lost) park_hit(cl, t, is0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -558,6 +579,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
     // ---- ordered fold by the group leader (raytrace_pixel's loop body, :136-158)
     uint32_t stop = 0;
+#if RRT_PROFILE
+    ++px_steps;
+#endif
     if (have && gl == 0) {
       const int n = n_step;
       spec ret = S(lget(gs.rr, gid), lget(gs.rg, gid), lget(gs.rb, gid));
@@ -584,7 +608,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       if (stop) {
         const uint32_t slot = lget(gs.slot, gid);
 #if RRT_PROFILE
-        atomicMax(&rrt_prof_slow[slot & 63u], ((wall_clock64() - t_claim) << 24) | (unsigned long long)(slot & 0xffffffu));
+        {  // elapsed wall ticks (26 bits) | rounds (7) | steps (7) | pixel slot (24)
+          const unsigned long long el = min(wall_clock64() - t_claim, (uint64_t)0x3ffffff);
+          atomicMax(&rrt_prof_slow[slot & 63u], (el << 38) | ((unsigned long long)min(px_rounds, 127u) << 31) |
+                                                    ((unsigned long long)min(px_steps, 127u) << 24) |
+                                                    (unsigned long long)(slot & 0xffffffu));
+        }
 #endif
         const spec r = ret / (float)i;
         kp.rgb[3 * slot] = r.r; kp.rgb[3 * slot + 1] = r.g; kp.rgb[3 * slot + 2] = r.b;

@@ -23,8 +23,10 @@ def constants(bh, lo, hi):
     steps = 0
     while steps * dt < 2 * np.pi:
         steps += 1
+    e = np.maximum(np.abs(lo - c), np.abs(hi - c))
+    r_ball = float(np.sqrt((e * e).sum())) * (1.0 + 1e-9)
     return dict(c=c, r=r, dt=dt, co=co, si=si, rho=rho, co1=co / rho, si1=si / rho, k15=1.5 * r,
-                scale=2.0 * sc, lo=lo, hi=hi, steps=steps)
+                scale=2.0 * sc, lo=lo, hi=hi, steps=steps, r_ball=r_ball)
 
 
 def _step0(K, o, d):
@@ -83,8 +85,9 @@ def run(K, o, d, step0_clear):
     ea = np.full(n, K["co1"])
     eb = np.full(n, K["si1"])
     sig = np.ones(n)
-    pp = p1
-    rp = np.sqrt(((p1 - K["c"]) ** 2).sum(1))
+    rp = K["rho"] / np.abs(vprev)
+    si2 = K["si"] * K["si"]
+    far_steps = 0
     with np.errstate(all="ignore"):
         for j in range(1, steps):
             sg = np.where(vprev < 0.0, -1.0, 1.0)
@@ -102,12 +105,19 @@ def run(K, o, d, step0_clear):
             na = a * ea - b * eb
             nb = a * eb + b * ea
             sig = sig * sg
-            iv = K["rho"] / v
-            p = K["c"] + (na * iv)[:, None] * X + (nb * iv)[:, None] * Y
-            r = np.abs(iv)
+            av, avp = np.abs(v), np.abs(vprev)
+            r = K["rho"] / av * (1.0 + 1e-6)
             m = ETA * (np.maximum(rp, r) + K["scale"])
-            alive &= seg_clear(pp, p, K["lo"], K["hi"], m)
+            rb = K["r_ball"] + m
+            D = v * v + vprev * vprev - 2.0 * K["co1"] * avp * v
+            inside = (v * (K["co1"] * avp - v) < 0.0) & (avp * (avp - K["co1"] * v) > 0.0)
+            far = np.where(inside, si2 > rb * rb * D, K["rho"] ** 2 > rb * rb * np.maximum(v * v, vprev * vprev))
+            pa = K["c"] + (ea * K["rho"] / vprev)[:, None] * X + (eb * K["rho"] / vprev)[:, None] * Y
+            p = K["c"] + (na * K["rho"] / v)[:, None] * X + (nb * K["rho"] / v)[:, None] * Y
+            alive &= far | seg_clear(pa, p, K["lo"], K["hi"], m)
+            far_steps += int((far & alive).sum())
             pts[j + 1] = np.where(alive[:, None], p, np.nan)
             mrg[j + 1] = np.where(alive, m, np.nan)
-            pp, rp, vprev, ea, eb = p, r, v, na, nb
+            rp, vprev, ea, eb = r, v, na, nb
+    run.far_steps = far_steps
     return alive, pts, mrg

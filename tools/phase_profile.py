@@ -70,10 +70,10 @@ def main():
         L.rrt_prof_read_slow(slow.ctypes.data)
         slow_px = []
         for v in sorted((int(x) for x in slow if x), reverse=True)[:16]:
-            sl, ticks = v & 0xffffff, v >> 24
+            sl, ticks = v & 0xffffff, v >> 38
             t_i, rr = sl // 1024, sl % 1024
             slow_px.append({"x": int(tiles[t_i][0]) + rr % 32, "y": int(tiles[t_i][1]) + rr // 32,
-                            "ms": ticks / (span / ms)})
+                            "ms": ticks / (span / ms), "rounds": (v >> 31) & 127, "steps": (v >> 24) & 127})
         out[fl] = {"kernel_ms": ms, "ticks_per_ms": span / ms, "waves": nw, "waves_with_work": int(res.sum()),
                    "exhausted_at": (tex - t0) / span, "wave_cycles": tot,
                    "camera_query": tq / tot, "micro_all": tm / tot, "camera_walk": tt / tot,
