@@ -467,25 +467,39 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     uint32_t mk = 0;            // slot of this lane's sample (lane gl = sample gl of the step)
     bool hk = false;
     int n_step = 0;             // samples the step resolves
-    for (;;) {
+    bool resolved = !have;      // (group-uniform)
+    for (int round = 0;; ++round) {
       const bool need = my < RRT_SLOTS;
       if (__ballot(need) == 0) break;
-      tail_prio();
+      if (round > 0) tail_prio();
 #if RRT_PROFILE
       ++prof_samples;
       ++px_rounds;
 #endif
+      bool h = false;
       if (need) {
         Isect is;
-        const bool h = slot_query(my, &is);
+        h = slot_query(my, &is);
         if (h) park_hit(cl, t, is);  // nothing of the hit stays live across later rounds
         held = my;
         lput(&gs.sst[gid][0], my, (uint8_t)(h ? 2 : 1));
         lput(&gs.sown[gid][0], my, (uint8_t)gl);
       }
+      if (round == 0) {  // the hypothesis held for every sample: the chain is its slots
+        const uint64_t comp = __ballot(need) & gmask, hb = __ballot(need && h) & gmask;
+        const bool hyp1 = lget(gs.hyp, gid) != 0;
+        if (!resolved && (int)__popcll(comp) == left && hb == (hyp1 ? comp : 0ull)) {
+          resolved = true;
+          n_step = left;
+          if (need) mk = my;
+          hk = h;
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      my = RRT_SLOTS;
+      if (resolved) continue;
       // walk the chain over the known slots (group-uniform)
       uint32_t m = 0;
       int k = 0, kh = 0;
@@ -499,8 +513,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         m += st >= 2 ? S1 : 1u;
       }
       n_step = k;
-      my = RRT_SLOTS;
       const bool open = have && k < left && m < RRT_SLOTS;  // unresolved samples remain
+      resolved = !open;
       // Lanes off the chain take the unknown slots along the continuation (an unknown slot taken
       // as the majority outcome of the resolved samples, the pixel's hypothesis before any):
       // first lanes whose slot needs no record (none, a miss, or a slot the chain has passed),
@@ -582,29 +596,35 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 #if RRT_PROFILE
     ++px_steps;
 #endif
+    // Adding a zero sample is an identity on the sums (ret, s1, s2 are never -0), and a step
+    // ends at the next adaptive check or at ns_aa, so its only possible stop is its last sample:
+    // the leader adds the nonzero samples in sample order and tests the stop once.
+    const uint64_t nonzero = __ballot(act && (s.r != 0.0f || s.g != 0.0f || s.b != 0.0f));
     if (have && gl == 0) {
       const int n = n_step;
       spec ret = S(lget(gs.rr, gid), lget(gs.rg, gid), lget(gs.rb, gid));
       double s1 = lget(gs.s1, gid), s2 = lget(gs.s2, gid);
-      int i = (int)lget(gs.i, gid);
-      uint32_t O = lget(gs.O, gid), hyp = 0;
-      for (int k = 0; k < n; ++k) {
+      int i = (int)lget(gs.i, gid) + n;
+      uint64_t nz = (nonzero >> gbase) & (n >= 64 ? ~0ull : ((1ull << n) - 1ull));
+      while (nz) {
+        const int k = (int)__builtin_ctzll(nz);
+        nz &= nz - 1;
         const spec sk = S(lget(fr, t + k), lget(fg, t + k), lget(fb, t + k));
         ret = ret + sk;
         const double il = illum(sk);
         s1 += il;
         s2 += il * il;
-        ++i;
-        const bool hk = (hits >> (gbase + k)) & 1ull;
-        O += hk ? Dh : Dm;
-        hyp = hk ? 1u : 0u;
-        bool st = i >= (int)kp.ns_aa;
-        if ((uint32_t)i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
-          const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
-          if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
-        }
-        if (st) { stop = 1; break; }
       }
+      const uint64_t hm = (hits >> gbase) & (n >= 64 ? ~0ull : ((1ull << n) - 1ull));
+      const uint32_t nh = (uint32_t)__popcll(hm);
+      const uint32_t O = lget(gs.O, gid) + nh * Dh + ((uint32_t)n - nh) * Dm;
+      const uint32_t hyp = n > 0 ? (uint32_t)((hm >> (n - 1)) & 1ull) : lget(gs.hyp, gid);
+      bool st = i >= (int)kp.ns_aa;
+      if ((uint32_t)i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
+        const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
+        if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
+      }
+      if (st) stop = 1;
       if (stop) {
         const uint32_t slot = lget(gs.slot, gid);
 #if RRT_PROFILE
