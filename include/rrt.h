@@ -168,13 +168,16 @@ enum {
                                      of the sample-parallel kernel (A/B testing) */
   RRT_RENDER_ORDERED = 1u << 9,   /* sample-parallel kernel: claim tiles in list order instead
                                      of centre-first (A/B testing) */
-  RRT_RENDER_NO_FIRST = 1u << 10, /* sample-parallel kernel: no sample-0 pre-pass (speculate
-                                     "miss" for a pixel's first step; A/B testing) */
+  RRT_RENDER_NO_FIRST = 1u << 10, /* sample-parallel kernel: no sample-0 pre-pass (the
+                                     default; overrides RRT_RENDER_PREPASS) */
   RRT_RENDER_ONE_QUEUE = 1u << 11, /* sample-parallel kernel: one chip-wide claim queue (A/B
                                      testing; results are identical) */
   RRT_RENDER_XCD_QUEUES = 1u << 12, /* sample-parallel kernel: one claim queue per XCD (A/B
                                      testing; results are identical).  Default: per-XCD queues
                                      for the general and Kerr builds, one queue for LEAN builds */
+  RRT_RENDER_PREPASS = 1u << 14, /* sample-parallel kernel: render sample 0 of every pixel in a
+                                     pre-pass whose hit status seeds the pixel's first hypothesis
+                                     (A/B testing; results are identical) */
   RRT_RENDER_NO_MISS_PROOF = 1u << 13, /* march every camera ray exactly instead of first trying
                                      the planar-recurrence miss proof (A/B testing; results
                                      are identical) */

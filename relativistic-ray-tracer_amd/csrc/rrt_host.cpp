@@ -1084,7 +1084,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
     kp.tile_order = c->d_order;
     kp.first = nullptr;
-    if (!(p->flags & RRT_RENDER_NO_FIRST)) {
+    // sample-0 pre-pass: off by default (with the slot speculation a wrong first hypothesis
+    // costs one round, less than the extra pass; tools/ab_kernels.py cfg3 46.4 vs 47.8 ms)
+    if ((p->flags & RRT_RENDER_PREPASS) && !(p->flags & RRT_RENDER_NO_FIRST)) {
       if (c->first_cap < kp.n_pixels) {
         hipFree(c->d_first); c->d_first = nullptr;
         HIPCHK(c, hipMalloc(&c->d_first, sizeof(KParams::FirstSample) * kp.n_pixels));

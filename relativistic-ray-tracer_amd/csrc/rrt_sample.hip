@@ -306,7 +306,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 #define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
 #endif
 
-#define RRT_SLOTS 64  // draw-offset slots per group and step
+// draw-offset slots per group and step: a hit takes Dh / Dm slots (2 with one area light, the
+// LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
+template <int LEAN>
+struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
 #ifndef RRT_TAIL_PRIO
 #define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
 #endif
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 
 // Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
 // run with only the lane's own few speculation registers live.
+template <uint32_t NSLOTS>
 struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   uint64_t key[32];
   uint32_t px[32], py[32], slot[32], O[32], i[32], hyp[32];
@@ -324,7 +328,7 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   // draw-offset slots of the current step (see the camera-query section): state 0 unknown,
   // 1 miss, 2 hit, 3 hit whose record was given up; owner = group lane whose ShadeLds slot holds
   // the hit record
-  uint8_t sst[32][RRT_SLOTS], sown[32][RRT_SLOTS];
+  uint8_t sst[32][NSLOTS], sown[32][NSLOTS];
 };
 
 template <int LEAN, int WAVES>
@@ -332,7 +336,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   const KParams& kp = *kpp;
   using namespace rrt;
   __shared__ ShadeLds cl;
-  __shared__ GroupLds gs;
+  constexpr uint32_t RRT_SLOTS = SlotWindow<LEAN>::n;
+  __shared__ GroupLds<RRT_SLOTS> gs;
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
   float* const fg = cl.cg;
   float* const fb = cl.cb;
