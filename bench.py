@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--traffic", default=None,
                     help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic; "
-                         "default profiles/r01_traffic.json (cfg3) or profiles/r01_traffic_<workload>.json")
+                         "default profiles/r02_traffic.json (cfg3) or profiles/r02_traffic_<workload>.json")
     a = ap.parse_args()
 
     import torch
@@ -226,8 +226,8 @@ def main():
     ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
     traffic = None
     if a.traffic is None:
-        a.traffic = os.path.join(ROOT, "profiles", "r01_traffic.json" if a.workload == "cfg3"
-                                 else f"r01_traffic_{a.workload}.json")
+        a.traffic = os.path.join(ROOT, "profiles", "r02_traffic.json" if a.workload == "cfg3"
+                                 else f"r02_traffic_{a.workload}.json")
     if os.path.exists(a.traffic):
         with open(a.traffic) as f:
             tr = json.load(f)

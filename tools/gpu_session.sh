@@ -27,6 +27,16 @@ for step in "$@"; do
     traffic) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run traffic 60 python3 tools/pmc_traffic.py ;;
+    traffic_all)  # PMC FETCH/WRITE per launch of the default kernels on cfg3 / cfg4 / cfg5 -> profiles/r02_traffic*.json
+           run pmc3_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc3_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
+           run pmc3_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc3_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
+           run traffic3 60 python3 tools/pmc_traffic.py --workload cfg3 --fetch gpurun_out/pmc3_fetch --write gpurun_out/pmc3_write --out gpurun_out/r02_traffic.json
+           run pmc4_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc4_fetch -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg4 --rounds 1 0
+           run pmc4_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4_write -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg4 --rounds 1 0
+           run traffic4 60 python3 tools/pmc_traffic.py --workload cfg4 --fetch gpurun_out/pmc4_fetch --write gpurun_out/pmc4_write --out gpurun_out/r02_traffic_cfg4.json
+           run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc5_fetch -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg5 --rounds 1 0
+           run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc5_write -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg5 --rounds 1 0
+           run traffic5 60 python3 tools/pmc_traffic.py --workload cfg5 --fetch gpurun_out/pmc5_fetch --write gpurun_out/pmc5_write --out gpurun_out/r02_traffic_cfg5.json ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-lean2:0:2 mega2:4:2}
