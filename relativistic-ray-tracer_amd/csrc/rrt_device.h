@@ -135,6 +135,7 @@ struct Counters {
   uint32_t bbox, micro, prim, query;
 #if RRT_PROFILE
   uint64_t t_micro, t_trav, t_query, t_proof, t_squery, t_strav;
+  uint64_t t_claim, t_chain, t_shade, t_fold;  // batch kernel phases
 #endif
 };
 #if RRT_PROFILE

@@ -111,8 +111,9 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 #if RRT_PROFILE
 // [0..7] per-phase wave cycles (busiest lane per wave, summed): total, camera queries, micro
 // steps, camera walks, miss proofs, shadow queries, shadow walks, -; [8] min start, [9] max end,
-// [10] waves, [11] first exhaustion (wall clock); then per-wave end / start / work records
-#define RRT_PROF_HDR 16
+// [10] waves, [11] first exhaustion (wall clock); [16..19] batch-kernel phases: claims, chain
+// walks, shading, fold; then per-wave end / start / work records
+#define RRT_PROF_HDR 24
 __device__ unsigned long long rrt_prof[RRT_PROF_HDR];
 __device__ unsigned long long rrt_prof_ends[16384], rrt_prof_starts[16384], rrt_prof_work[16384];
 // slowest pixels: bucket (pixel slot % 64) keeps max(elapsed wall ticks << 24 | slot)
@@ -129,7 +130,7 @@ extern "C" int rrt_prof_read(unsigned long long* out) {  // out: RRT_PROF_HDR + 
     return -1;
   if (hipMemcpyFromSymbol(out + RRT_PROF_HDR + 2 * 16384, HIP_SYMBOL(rrt_prof_work), sizeof(rrt_prof_work)) != hipSuccess)
     return -1;
-  unsigned long long z[RRT_PROF_HDR] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, ~0ull};
+  unsigned long long z[RRT_PROF_HDR] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, ~0ull, 0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(rrt_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
@@ -363,19 +364,44 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
   for (;;) {
     // ---- claim a pixel (one atomic per group)
-    if (!have && !done) {
-      uint32_t p = 0;
-      if (gl == 0) {  // this XCD's queue first, then the others in turn (KParams::q_end)
-        for (;;) {
-          const uint32_t qb = q ? kp.q_end[q - 1] : 0u;
-          const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, 1u);
-          if (k < kp.q_end[q] - qb) { p = qb + k; break; }
-          if (--q_left == 0) { p = kp.n_pixels; break; }
-          q = q + 1 == kp.n_queues ? 0u : q + 1;
+    RRT_T0(tc0);
+    // The wave's group leaders that need a pixel claim together: one atomic takes as many
+    // consecutive claims as there are leaders (2 with the BASELINE group size), lane 0 issues it.
+    const uint64_t needers = __ballot(gl == 0 && !have && !done);
+    if (needers) {
+      uint64_t pending = needers;
+      uint32_t p = kp.n_pixels + 1;  // n_pixels + 1: this group did not claim
+      while (pending) {
+        const uint32_t want = (uint32_t)__popcll(pending);
+        uint32_t base = 0, got = 0, out = 0;
+        if (lane == 0) {  // this XCD's queue first, then the others in turn (KParams::q_end)
+          if (q_left == 0) {  // every queue found empty before
+            out = 1;
+          } else {
+            const uint32_t qb = q ? kp.q_end[q - 1] : 0u, qn = kp.q_end[q] - qb;
+            const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, want);
+            if (k < qn) {
+              base = qb + k; got = min(want, qn - k);
+            } else if (--q_left == 0) {
+              out = 1;
+            } else {
+              q = q + 1 == kp.n_queues ? 0u : q + 1;
+            }
+          }
         }
+        base = __shfl(base, 0); got = __shfl(got, 0); out = __shfl(out, 0);
+        const uint32_t rank = (uint32_t)__popcll(pending & ((1ull << gbase) - 1ull));  // pending leaders before mine
+        const bool mine = (pending >> gbase) & 1ull;
+        if (mine && rank < got) p = base + rank;
+        if (mine && out) p = kp.n_pixels;
+        pending = out ? 0ull : (got >= want ? 0ull : pending & ~__ballot(gl == 0 && mine && rank < got));
       }
+      q = __shfl(q, 0);
+      q_left = __shfl(q_left, 0);
       p = __shfl(p, (int)gbase);
-      if (p >= kp.n_pixels) {
+      if (p == kp.n_pixels + 1) {
+        // (the group kept its pixel)
+      } else if (p >= kp.n_pixels) {
         done = true;
 #if RRT_PROFILE
         if (gl == 0) atomicMin(&rrt_prof[11], (unsigned long long)wall_clock64());
@@ -414,6 +440,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         }
       }
     }
+    RRT_ACC(t_claim, tc0);
     if (__ballot(!done) == 0) break;
     // Tail latency: a pixel whose rounds are long (the costliest ones -- long walks next to the
     // hole and the geometry) keeps its wave busy long after the claim queue runs dry.  A wave
@@ -505,6 +532,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       my = RRT_SLOTS;
       if (resolved) continue;
+      RRT_T0(tw0);
       // walk the chain over the known slots (group-uniform)
       uint32_t m = 0;
       int k = 0, kh = 0;
@@ -543,6 +571,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         }
         if (my < RRT_SLOTS && free_b) lput(&gs.sst[gid][0], held, (uint8_t)3);
       }
+      RRT_ACC(t_chain, tw0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -573,6 +602,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     const uint64_t hits = __ballot(hit);
 
     // ---- shading (est_radiance_global_illumination, :103-123), all samples in parallel
+    RRT_T0(ts0);
     spec s = S(0, 0, 0);
     if (!is_lean(LEAN) && act && !hit && kp.env.w) {  // miss: envLight->sample_dir of the unbent camera ray
       Rng g; g.key = lget(gs.key, gid); g.ctr = off;  // re-derive the ray from its jitter draws
@@ -596,7 +626,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    RRT_ACC(t_shade, ts0);
     // ---- ordered fold by the group leader (raytrace_pixel's loop body, :136-158)
+    RRT_T0(tf0);
     uint32_t stop = 0;
 #if RRT_PROFILE
     ++px_steps;
@@ -652,16 +684,18 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     }
     stop = __shfl(stop, (int)gbase);
     if (stop) have = false;
+    RRT_ACC(t_fold, tf0);
   }
 #if RRT_PROFILE
   const uint64_t t_end = clock64(), w_end = wall_clock64();
-  uint64_t v[8] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0};
-  for (int k = 0; k < 8; ++k) {
+  uint64_t v[12] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0,
+                    cn.t_claim, cn.t_chain, cn.t_shade, cn.t_fold};
+  for (int k = 0; k < 12; ++k) {
     for (int off2 = 32; off2 > 0; off2 >>= 1) {
       const uint64_t o2 = __shfl_xor(v[k], off2);
       v[k] = v[k] > o2 ? v[k] : o2;
     }
-    if (lane == 0) atomicAdd(&rrt_prof[k], (unsigned long long)v[k]);
+    if (lane == 0) atomicAdd(&rrt_prof[k < 8 ? k : k + 8], (unsigned long long)v[k]);
   }
   uint32_t nb = gl == 0 ? prof_blocks : 0;
   for (int off2 = 32; off2 > 0; off2 >>= 1) nb += __shfl_xor(nb, off2);

@@ -41,7 +41,7 @@ def main():
     n = len(tiles) * 1024
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
-    HDR = 16
+    HDR = 24
     buf = np.zeros(HDR + 3 * 16384, np.uint64)
     out = {}
     for fl in a.flags:
@@ -79,6 +79,8 @@ def main():
                    "camera_query": tq / tot, "micro_all": tm / tot, "camera_walk": tt / tot,
                    "miss_proof": tp / tot, "shadow_query": tsq / tot, "shadow_walk": tst / tot,
                    "outside_queries_and_proof": 1 - (tq + tp + tsq) / tot,
+                   "claim": float(buf[16]) / tot, "chain": float(buf[17]) / tot, "shade_incl_shadow": float(buf[18]) / tot,
+                   "fold": float(buf[19]) / tot,
                    "slowest_pixels": slow_px,
                    "busy_frac_working_waves": float(((ends - starts)[res]).sum() / max(res.sum(), 1)),
                    "working_wave_end_q": [round(float(q), 3) for q in np.quantile(ends[res], [0.05, 0.25, 0.5, 0.75, 0.95, 1.0])],
