@@ -175,6 +175,9 @@ enum {
   RRT_RENDER_XCD_QUEUES = 1u << 12, /* sample-parallel kernel: one claim queue per XCD (A/B
                                      testing; results are identical).  Default: per-XCD queues
                                      for the general and Kerr builds, one queue for LEAN builds */
+  RRT_RENDER_STRIPED_QUEUES = 1u << 15, /* sample-parallel kernel: the centre-first claim order
+                                     dealt round-robin over one claim counter per XCD (A/B;
+                                     the default of the area/point-light builds) */
   RRT_RENDER_PREPASS = 1u << 14, /* sample-parallel kernel: render sample 0 of every pixel in a
                                      pre-pass whose hit status seeds the pixel's first hypothesis
                                      (A/B testing; results are identical) */

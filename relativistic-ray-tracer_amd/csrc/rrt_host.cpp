@@ -1047,8 +1047,14 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     const bool ordered = p->flags & RRT_RENDER_ORDERED;
     // A/B (profiles/r01_queues_ab.md): per-XCD queues cost the LEAN cfg3 build 6% and save the
     // Kerr cfg5 build 2%, so they are the default for the general / Kerr builds only
-    const bool xcd_q = (p->flags & RRT_RENDER_XCD_QUEUES) || ((lean == 0 || lean == 3) && !(p->flags & RRT_RENDER_ONE_QUEUE));
-    const uint32_t nq = (ordered || !xcd_q) ? 1u : RRT_MAX_QUEUES;
+    const bool xcd_q = (p->flags & RRT_RENDER_XCD_QUEUES) || ((lean == 0 || lean == 3) && !(p->flags & RRT_RENDER_ONE_QUEUE) &&
+                                                             !(p->flags & RRT_RENDER_STRIPED_QUEUES));
+    // Striped queues (the LEAN default): the centre-first order dealt round-robin over one
+    // counter per XCD, so the claim atomics spread over 8 addresses while the order stays global
+    const bool striped = !ordered && !(p->flags & RRT_RENDER_ONE_QUEUE) && !(p->flags & RRT_RENDER_XCD_QUEUES) &&
+                         ((p->flags & RRT_RENDER_STRIPED_QUEUES) || lean == 1 || lean == 2);
+    const uint32_t nq = (ordered || !(xcd_q || striped)) ? 1u : RRT_MAX_QUEUES;
+    kp.q_stripe = striped ? 1u : 0u;
     std::vector<uint32_t> sector(n_tiles, 0);
     if (!ordered) {
       const double cx = 0.5 * p->frame_w, cy = 0.5 * p->frame_h;
@@ -1056,7 +1062,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       for (uint32_t k = 0; k < n_tiles; ++k) {
         const double dx = tiles[2 * k] + 0.5 * ts - cx, dy = tiles[2 * k + 1] + 0.5 * ts - cy;
         key[k] = dx * dx + dy * dy;
-        if (nq > 1) {
+        if (nq > 1 && !striped) {
           const double a = std::atan2(dy, dx) + kPI;  // [0, 2 pi]
           sector[k] = std::min<uint32_t>((uint32_t)(a * (nq / (2 * kPI))), nq - 1);
         }

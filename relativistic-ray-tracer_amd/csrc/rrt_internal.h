@@ -160,6 +160,7 @@ struct KParams {
   // its counter is block_counter[RRT_QUEUE_STRIDE * q]; a block starts on queue blockIdx % n_queues
   uint32_t n_queues;
   uint32_t q_end[RRT_MAX_QUEUES];
+  uint32_t q_stripe;     // 1: queue q holds claims q, q + n_queues, ... of the whole order (q_end unused)
   struct FirstSample { float r, g, b; uint32_t hit; };
   FirstSample* first;          // sample 0 of every pixel slot (rrt_first_kernel), or null
   uint32_t group;        // lanes per pixel (power of two, 2..32)

@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
 template <int LEAN>
 struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
+#define RRT_STRIPE 16  // striped claim queues: runs of consecutive claims (neighbouring pixels)
 #ifndef RRT_TAIL_PRIO
 #define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
 #endif
@@ -373,26 +374,34 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       uint32_t p = kp.n_pixels + 1;  // n_pixels + 1: this group did not claim
       while (pending) {
         const uint32_t want = (uint32_t)__popcll(pending);
-        uint32_t base = 0, got = 0, out = 0;
+        uint32_t base = 0, got = 0, out = 0, qc = 0;
         if (lane == 0) {  // this XCD's queue first, then the others in turn (KParams::q_end)
           if (q_left == 0) {  // every queue found empty before
             out = 1;
           } else {
-            const uint32_t qb = q ? kp.q_end[q - 1] : 0u, qn = kp.q_end[q] - qb;
+            // striped queues: queue q holds the runs q, q + nq, q + 2 nq, ... of RRT_STRIPE
+            // consecutive claims (n_pixels is a multiple of 64: tiles of 8k x 8k pixels)
+            const uint32_t nq = kp.n_queues;
+            const uint32_t qb = kp.q_stripe ? 0u : (q ? kp.q_end[q - 1] : 0u);
+            const uint32_t qn = kp.q_stripe ? (kp.n_pixels / RRT_STRIPE - q + nq - 1) / nq * RRT_STRIPE
+                                            : kp.q_end[q] - qb;
             const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, want);
             if (k < qn) {
-              base = qb + k; got = min(want, qn - k);
+              base = qb + k; got = min(want, qn - k); qc = q;
             } else if (--q_left == 0) {
               out = 1;
             } else {
-              q = q + 1 == kp.n_queues ? 0u : q + 1;
+              q = q + 1 == nq ? 0u : q + 1;
             }
           }
         }
-        base = __shfl(base, 0); got = __shfl(got, 0); out = __shfl(out, 0);
+        base = __shfl(base, 0); got = __shfl(got, 0); out = __shfl(out, 0); qc = __shfl(qc, 0);
         const uint32_t rank = (uint32_t)__popcll(pending & ((1ull << gbase) - 1ull));  // pending leaders before mine
         const bool mine = (pending >> gbase) & 1ull;
-        if (mine && rank < got) p = base + rank;
+        if (mine && rank < got) {
+          const uint32_t ix = base + rank;
+          p = kp.q_stripe ? ((ix / RRT_STRIPE) * kp.n_queues + qc) * RRT_STRIPE + ix % RRT_STRIPE : ix;
+        }
         if (mine && out) p = kp.n_pixels;
         pending = out ? 0ull : (got >= want ? 0ull : pending & ~__ballot(gl == 0 && mine && rank < got));
       }

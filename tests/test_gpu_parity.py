@@ -58,7 +58,7 @@ def check(c, rgb, cnt, draws):
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "xcdqueues": rrt.RRT_RENDER_XCD_QUEUES,
             "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
-            "prepass": rrt.RRT_RENDER_PREPASS,
+            "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "wavefront": rrt.RRT_RENDER_WAVEFRONT}
 
