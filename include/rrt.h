@@ -148,8 +148,9 @@ typedef struct {
   uint64_t seed;              /* keyed RNG seed */
   uint32_t frame_w, frame_h;  /* sampleBuffer.w / h (set_frame_size) */
   uint32_t flags;             /* RRT_RENDER_* */
-  uint32_t variant;           /* 0 = default; 1..5 = waves/SIMD the depth<=1 kernel is built
-                                 for (register budget), for A/B measurements */
+  uint32_t variant;           /* A/B measurements, 0 = defaults.  Bits 0..7: waves/SIMD the
+                                 depth<=1 kernel is built for (1..6, register budget); bits
+                                 8..11: the sample-0 pre-pass's waves/SIMD */
 } rrt_render_params;
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
@@ -184,6 +185,9 @@ enum {
   RRT_RENDER_NO_MISS_PROOF = 1u << 13, /* march every camera ray exactly instead of first trying
                                      the planar-recurrence miss proof (A/B testing; results
                                      are identical) */
+  RRT_RENDER_NO_SHADOW_PROOF = 1u << 16, /* march every shadow ray exactly instead of first trying
+                                     the occlusion proof (a certain crossing of a root-box face
+                                     triangle before any possible capture; A/B and parity) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of
@@ -264,6 +268,12 @@ int rrt_get_free_grid(const rrt_ctx* ctx, uint8_t* k, double* geom, int32_t* n);
  * primitive within reach; *reach = the segment length below which a clear bit lets the walk skip
  * that leaf.  Returns the number of cells (0 = no masks).  Host-side tests. */
 int rrt_get_big_masks(const rrt_ctx* ctx, uint32_t* mask, double* reach);
+/* The shadow-ray occlusion proof's triangles: per root-box face f (axis f % 3;
+ * the low face for f < 3, else the high face) up to 4 triangles lying along it, each as 16
+ * doubles: unit plane normal n (toward the box's inside) and offset d, then the three in-plane
+ * inward unit edge normals en[3][3] and their offsets eo[3]: tris [6][4][16], counts [6].
+ * Returns the total (0 = the proof never applies).  Any pointer may be NULL.  Host-side tests. */
+int rrt_get_occluders(const rrt_ctx* ctx, double* tris, uint32_t* counts);
 
 /* ---------------------------------------------------------------- file helpers (.rrts/.rrtc) */
 typedef struct rrt_scene_file rrt_scene_file;

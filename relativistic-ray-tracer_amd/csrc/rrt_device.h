@@ -760,6 +760,130 @@ __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect*
   return false;
 }
 
+// ------------------------------------------------------------------ shadow-ray occlusion proof
+#ifndef RRT_SHADOW_PROOF
+#define RRT_SHADOW_PROOF 1  // 0: build without the occlusion proof (A/B)
+#endif
+// (DESIGN.md §5).  The reference's shadow query (bvh.cpp:103-113; the caller uses only the
+// boolean) is true iff some micro segment before the capture hits a primitive.  Most shadow rays
+// of a closed room end on a wall, after ~15-30 exact steps and walks.  The proof marches the
+// camera proof's recurrence from the shadow ray itself: every segment must clear the
+// capture sphere by the margin m, and once a segment end leaves the trigger box (the root box
+// shrunk past the wall triangles kept by rrt_host.cpp build_occluders) the segment must cross one
+// of those triangles with margin -- end points m beyond its plane on either side, the crossing
+// point mq inside every edge.  The reference's segment then crosses it too, its triangle test
+// accepts (triangle.cpp:25-55) and the leaf boxes on the way pass, so the query returns true.
+// Anything else (an end point near a wall, a face without triangles, a cancelling step, the
+// march ending) is no proof: the caller marches exactly.
+// A certain crossing of a triangle of face f by the segment a -> b: end points more than m on
+// either side of its plane (either way), the crossing point mq inside every edge.
+__device__ __forceinline__ bool occ_face(const DShadowProof& sp, int f, v3 a, v3 b, double m) {
+#pragma clang fp contract(fast)
+#pragma unroll 1
+  for (uint32_t i = 0; i < sp.n[f]; ++i) {
+    const DOccluder& t = sp.tri[f][i];
+    const double da = t.n[0] * a.x + t.n[1] * a.y + t.n[2] * a.z - t.d;
+    const double db = t.n[0] * b.x + t.n[1] * b.y + t.n[2] * b.z - t.d;
+    if (!((da > m && db < -m) || (da < -m && db > m))) continue;
+    const double tq = da / (da - db);
+    const v3 q = V(a.x + (b.x - a.x) * tq, a.y + (b.y - a.y) * tq, a.z + (b.z - a.z) * tq);
+    // end points within m of the reference's move the crossing by <= m (2 + |b - a| / |da - db|)
+    const double mq = m * (2.0 + (fabs(b.x - a.x) + fabs(b.y - a.y) + fabs(b.z - a.z)) / fabs(da - db));
+    bool in = true;
+    for (int k = 0; k < 3; ++k) in = in && t.en[k][0] * q.x + t.en[k][1] * q.y + t.en[k][2] * q.z - t.eo[k] >= mq;
+    if (in) return true;
+  }
+  return false;
+}
+// The segment a -> b with an end outside the trigger box: 1 = a certain crossing of a triangle of
+// a face that an end is past; -1 = no proof and b has left the root box (the ray leaves the room:
+// give up); 0 = go on.  Loops kept rolled: this runs once or twice per shadow ray.
+__device__ __forceinline__ int occ_exit(const KParams& kp, v3 a, v3 b, double m) {
+  const DShadowProof& sp = kp.occ;
+  bool out = false;
+#pragma unroll 1
+  for (int f = 0; f < 6; ++f) {
+    const int k = f < 3 ? f : f - 3;
+    const double ak = k == 0 ? a.x : k == 1 ? a.y : a.z, bk = k == 0 ? b.x : k == 1 ? b.y : b.z;
+    const bool past = f < 3 ? !(bk >= sp.in_lo[k] && ak >= sp.in_lo[k]) : !(bk <= sp.in_hi[k] && ak <= sp.in_hi[k]);
+    if (past && occ_face(sp, f, a, b, m)) return 1;
+    out = out || !(f < 3 ? bk >= kp.miss.lo[k] : bk <= kp.miss.hi[k]);  // NaN: out
+  }
+  return out ? -1 : 0;
+}
+#ifndef RRT_SHADOW_MODE
+#define RRT_SHADOW_MODE 2  // A/B: 0 inline; 1 the whole proof out of line; 2 occ_exit out of line
+#endif
+template <int W>
+__device__ __noinline__ int occ_exit_call(const KParams& kp, v3 a, v3 b, double m) { return occ_exit(kp, a, b, m); }
+__device__ __forceinline__ bool occ_inside(const DShadowProof& sp, v3 b) {
+  return b.x >= sp.in_lo[0] && b.x <= sp.in_hi[0] && b.y >= sp.in_lo[1] && b.y <= sp.in_hi[1] && b.z >= sp.in_lo[2] &&
+         b.z <= sp.in_hi[2];
+}
+// The whole march by the recurrence, step 0 included: the ray (o, d) is the state of a step from
+// the point A = o itself (|A - c| = 1 / u, so v_prev = rho u, E_prev = x, s_prev chosen so the
+// update yields s = u and the reference's u' = -u (d . x) / |d - (d . x) x|).
+template <int W = 0>
+__device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v3 d, int steps) {
+#pragma clang fp contract(fast)
+  const DMissProof& mp = kp.miss;
+  const DShadowProof& sp = kp.occ;
+  const DHole& h = kp.hole;
+  const v3 c = V(h.c[0], h.c[1], h.c[2]);
+  const v3 x0 = o - c;
+  const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
+  const v3 X = vmul(x0, u0);
+  const double dx = dot(d, X);
+  v3 Y = d - smul(dx, X);
+  const double dy = sqrt(norm2(Y));
+  Y = vmul(Y, 1.0 / dy);
+  const double up0 = -u0 * dx / dy;
+  double vprev = mp.rho * u0, s = u0 * mp.co1 - up0 * h.sin_dt * mp.inv_rho;
+  double ea = 1.0, eb = 0.0, sig = 1.0, rp = r0;
+  bool a_in = occ_inside(sp, o);
+  const double si2 = h.sin_dt * h.sin_dt, rc = h.r * (1.0 + 1e-9);
+#pragma unroll 1
+  for (int j = 0; j < steps; ++j) {
+    const double sg = vprev < 0.0 ? -1.0 : 1.0;
+    const double up = (vprev * mp.co1 - mp.rho * s) * mp.inv_si;
+    s = fabs(vprev) * mp.inv_rho;
+    const double f1 = -s + mp.k15 * s * s;
+    const double u2 = s + up * (h.dt * 0.5);
+    const double f2 = -u2 + mp.k15 * u2 * u2;
+    const double u3 = u2 + f1 * mp.dt2_4;
+    const double f3 = -u3 + mp.k15 * u3 * u3;
+    const double v = s + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
+    if (!(fabs(v) >= mp.kappa * (s + fabs(up) * h.dt))) return false;  // cancelling step (or NaN)
+    const double a = sg * mp.co1, b = sig * mp.si1;
+    const double na = a * ea - b * eb, nb = a * eb + b * ea;
+    sig *= sg;
+    const double av = fabs(v), avp = fabs(vprev);
+    const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);  // |B - c| (upper bound)
+    const double m = mp.eta * (fmax(rp, r) + mp.scale);
+    // the segment must clear the capture sphere: its distance from the hole > r_s + m (the
+    // camera proof's scalar distance: foot of the perpendicular inside, else the nearer end)
+    const double rb = rc + m;
+    const double D = v * v + vprev * vprev - 2.0 * mp.co1 * avp * v;
+    const bool inside = v * (mp.co1 * avp - v) < 0.0 && avp * (avp - mp.co1 * v) > 0.0;
+    const bool clear = inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(v * v, vprev * vprev);
+    if (!clear) return false;
+    const double ib = mp.rho / v;
+    const v3 pb = V(c.x + (na * ib) * X.x + (nb * ib) * Y.x, c.y + (na * ib) * X.y + (nb * ib) * Y.y,
+                    c.z + (na * ib) * X.z + (nb * ib) * Y.z);
+    const bool b_in = occ_inside(sp, pb);
+    if (!b_in || !a_in) {
+      const double ia = mp.rho / vprev;
+      const v3 pa = V(c.x + (ea * ia) * X.x + (eb * ia) * Y.x, c.y + (ea * ia) * X.y + (eb * ia) * Y.y,
+                      c.z + (ea * ia) * X.z + (eb * ia) * Y.z);
+      const int res = RRT_SHADOW_MODE == 2 ? occ_exit_call<W>(kp, pa, pb, m) : occ_exit(kp, pa, pb, m);
+      if (res) return res > 0;
+    }
+    a_in = b_in;
+    rp = r; vprev = v; ea = na; eb = nb;
+  }
+  return false;
+}
+
 // BVHAccel::intersect (bvh.cpp:103-113): march the geodesic as straight micro segments; the
 // incoming ray's min_t / max_t are dropped (camera clip planes and shadow-ray distance are
 // ignored, as in the reference).  Capture by the hole returns "no hit".  KERR: the Kerr build
@@ -913,8 +1037,27 @@ __device__ __noinline__ bool query_call(const KParams& kp, v3 o, v3 d, Isect* is
   Counters cn = {};
   return query<ANY, false, KERR>(kp, o, d, is, cn);
 }
-template <bool ANY, bool COUNT, bool NI, bool KERR = false>
+// The occlusion proof's build tag W (0: no proof in this build).  Its out-of-line parts (the
+// face test, or the whole proof in mode 1) get one copy per calling kernel build: a callee shared
+// by kernels of different waves-per-SIMD budgets gets the smallest budget's registers, and every
+// caller then allocates the callee's count.  Measured on cfg3 (profiles/r02_ab_log.md): inline
+// 31.5 ms, face test out of line 31.3, whole proof out of line 37.6 (the call's frame and SGPR
+// saves), no proof 35.3.
+template <int W>
+__device__ __noinline__ bool shadow_proof_call(const KParams& kp, v3 o, v3 d) {
+  return shadow_occluded_proof(kp, o, d, kp.hole.steps);
+}
+// W: the occlusion proof's build tag (0: none)
+template <bool ANY, bool COUNT, bool NI, bool KERR = false, int W = 0>
 __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  // shadow rays: the occlusion proof first (Schwarzschild; never in the reference-work counts)
+  if (RRT_SHADOW_PROOF && W && ANY && !KERR && kp.occ.on && !(COUNT && !kp.count_exec)) {
+    RRT_T0(tp0);
+    const bool occluded = RRT_SHADOW_MODE == 1 ? shadow_proof_call<W>(kp, o, d)
+                                               : shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
+    RRT_ACC(t_squery, tp0);
+    if (occluded) return true;
+  }
   if (NI && !COUNT) return query_call<ANY, KERR>(kp, o, d, is);
   return query<ANY, COUNT, KERR>(kp, o, d, is, cn);
 }

@@ -41,6 +41,7 @@ struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
 inline V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 inline V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline double get(V3 a, int k) { return k == 0 ? a.x : k == 1 ? a.y : a.z; }
 inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
 inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
 
@@ -132,6 +133,7 @@ struct rrt_ctx {
   std::vector<DNode> clean;  // host copies (rrt_get_clean_tree)
   std::vector<DBig> big;
   std::vector<uint32_t> big_mask;   // build_big_masks (host copy; rrt_get_big_masks)
+  DShadowProof occ{};               // build_occluders (the root box's face triangles)
   uint32_t* d_big_mask = nullptr;
   uint64_t device_bytes = 0;
   // per-launch workspace
@@ -347,6 +349,76 @@ static bool grid_mark_leaf(const rrt_ctx* c, const double g0[3], double h, const
         }
   }
   return true;
+}
+
+// Shadow-ray occlusion proof (rrt_device.h shadow_occluded_proof): the large triangles within 1%
+// of the scene's extent of a root-box face and facing along its axis (walls; CBempty's back wall
+// sits 0.2% inside the box), taken as the reference intersects them (p0, p0 + e1, p0 + e2),
+// largest first, RRT_OCC_PER_FACE per face, none under 5% of the face's largest: plane (normal
+// toward the box's inside) and in-plane edge normals.  Any triangle of the scene would do (a certain crossing of any of them is
+// a reference hit); these are the ones a shadow ray leaving a closed room crosses last.
+static void build_occluders(rrt_ctx* c) {
+  DShadowProof& o = c->occ;
+  o = DShadowProof{};
+  if (c->nodes.empty()) return;
+  const Box& rb = c->nodes[0].bb;
+  const double lo[3] = {rb.mn.x, rb.mn.y, rb.mn.z}, hi[3] = {rb.mx.x, rb.mx.y, rb.mx.z};
+  double sc = 0.0;
+  for (int k = 0; k < 3; ++k) sc = std::max(sc, hi[k] - lo[k]);
+  if (!(sc > 0.0) || !std::isfinite(sc)) return;
+  const double tol = 1e-2 * sc;
+  struct Cand { double area, w; DOccluder t; };
+  std::vector<Cand> cand[6];
+  for (const Prim& p : c->prims) {
+    if (p.kind != RRT_OBJ_MESH) continue;
+    const V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
+    const V3 q[3] = {p0, add(p0, e1), add(p0, e2)};
+    const V3 nn = mk(e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x);
+    const double nl = std::sqrt(nn.x * nn.x + nn.y * nn.y + nn.z * nn.z);
+    if (!(nl > 0.0) || !std::isfinite(nl)) continue;
+    for (int f = 0; f < 6; ++f) {
+      const int k = f % 3;
+      const double face = f < 3 ? lo[k] : hi[k];
+      double w = 0.0;
+      for (const V3& v : q) w = std::max(w, std::fabs(get(v, k) - face));
+      if (!(w <= tol)) continue;
+      DOccluder t{};
+      // plane normal toward the inside of the box (+axis on a low face, -axis on a high face)
+      double s = (get(nn, k) >= 0.0) == (f < 3) ? 1.0 / nl : -1.0 / nl;
+      const V3 n = mk(nn.x * s, nn.y * s, nn.z * s);
+      if (!(std::fabs(get(n, k)) > 0.5)) continue;  // not facing along the axis
+      t.n[0] = n.x; t.n[1] = n.y; t.n[2] = n.z;
+      t.d = n.x * p0.x + n.y * p0.y + n.z * p0.z;
+      bool ok = true;
+      for (int i = 0; i < 3 && ok; ++i) {
+        const V3 a = q[i], b = q[(i + 1) % 3];
+        const V3 e = sub(b, a);
+        // inward in-plane normal of edge a -> b: (e1 x e2) x e for the counter-clockwise winding
+        V3 m = mk(nn.y * e.z - nn.z * e.y, nn.z * e.x - nn.x * e.z, nn.x * e.y - nn.y * e.x);
+        const double ml = std::sqrt(m.x * m.x + m.y * m.y + m.z * m.z);
+        if (!(ml > 0.0) || !std::isfinite(ml)) { ok = false; break; }
+        m = mk(m.x / ml, m.y / ml, m.z / ml);
+        t.en[i][0] = m.x; t.en[i][1] = m.y; t.en[i][2] = m.z;
+        t.eo[i] = m.x * a.x + m.y * a.y + m.z * a.z;
+      }
+      // the opposite vertex must be inside each edge (a proper, non-degenerate triangle)
+      for (int i = 0; i < 3 && ok; ++i) {
+        const V3 v = q[(i + 2) % 3];
+        ok = t.en[i][0] * v.x + t.en[i][1] * v.y + t.en[i][2] * v.z - t.eo[i] > 0.0;
+      }
+      if (ok) cand[f].push_back({0.5 * nl, w, t});
+    }
+  }
+  for (int f = 0; f < 6; ++f) {
+    std::stable_sort(cand[f].begin(), cand[f].end(), [](const Cand& x, const Cand& y) { return x.area > y.area; });
+    size_t keep = std::min<size_t>(cand[f].size(), RRT_OCC_PER_FACE);
+    while (keep > 1 && cand[f][keep - 1].area < 0.05 * cand[f][0].area) --keep;
+    o.n[f] = (uint32_t)keep;
+    for (uint32_t i = 0; i < o.n[f]; ++i) {
+      o.tri[f][i] = cand[f][i].t;
+      o.w[f] = std::max(o.w[f], cand[f][i].w);
+    }
+  }
 }
 
 static void build_free_grid(rrt_ctx* c) {
@@ -697,6 +769,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
     }
   }
   build_free_grid(c);
+  build_occluders(c);
   build_clean_tree(c, c->clean, c->big);
   build_big_masks(c);
   {  // plane-cull margin: 1e-9 of the scene's coordinate scale (rounding is ~1e-16 of it)
@@ -973,6 +1046,20 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     mp.on = (h.kind == RRT_METRIC_SCHWARZSCHILD && fin && h.dt > 0.0 && h.dt < 3.0 && h.sin_dt > 0.0 &&
              h.steps >= 1 && !(p->flags & RRT_RENDER_NO_MISS_PROOF))
                 ? 1u : 0u;
+  }
+  {  // shadow-ray occlusion proof: the same recurrence, against the root box's face triangles
+    kp.occ = c->occ;
+    uint32_t any = 0;
+    for (int f = 0; f < 6; ++f) any += kp.occ.n[f];
+    const bool fin = std::isfinite(kp.miss.scale) && std::isfinite(kp.hole.r) && kp.hole.r >= 0.0;
+    // trigger box: the root box shrunk past every kept triangle by twice the largest margin
+    // the proof uses inside the box, eta (r_ball + scale)
+    const double m2 = 2.0 * kp.miss.eta * (kp.miss.r_ball + kp.miss.scale);
+    for (int k = 0; k < 3; ++k) {
+      kp.occ.in_lo[k] = kp.miss.lo[k] + kp.occ.w[k] + m2;
+      kp.occ.in_hi[k] = kp.miss.hi[k] - kp.occ.w[k + 3] - m2;
+    }
+    kp.occ.on = (kp.miss.on && any && fin && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
   }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
@@ -1272,6 +1359,17 @@ extern "C" int rrt_get_free_grid(const rrt_ctx* c, uint8_t* k, double* geom, int
   }
   if (n) for (int i = 0; i < 3; ++i) n[i] = c->hgrid.n[i];
   return (int)std::min<size_t>(c->grid.size(), 0x7fffffff);
+}
+
+extern "C" int rrt_get_occluders(const rrt_ctx* c, double* tris, uint32_t* counts) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  int total = 0;
+  for (int f = 0; f < 6; ++f) {
+    if (counts) counts[f] = c->occ.n[f];
+    if (tris) std::memcpy(tris + 16 * RRT_OCC_PER_FACE * f, c->occ.tri[f], sizeof(c->occ.tri[f]));
+    total += (int)c->occ.n[f];
+  }
+  return total;
 }
 
 extern "C" int rrt_get_big_masks(const rrt_ctx* c, uint32_t* mask, double* reach) {

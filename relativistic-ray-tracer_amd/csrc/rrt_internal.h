@@ -112,6 +112,23 @@ struct DMissProof {
   uint32_t on, pad;
 };
 
+// Shadow-ray occlusion proof (rrt_device.h shadow_occluded_proof): triangles that
+// lie along the root box's faces (a Cornell box's walls), as the reference intersects them
+// (p0, p0 + e1, p0 + e2).  Face f: axis f % 3, the box's low face for f < 3, else its high face.
+// n . x - d: signed distance from the triangle's plane, positive on the box's inner side;
+// en[i] . x - eo[i]: distance inside edge i within the plane (unit, inward).  A segment end past
+// the trigger box [in_lo, in_hi] (the root box shrunk past every kept triangle by a margin) is
+// tested against the triangles of the faces it is past.
+#define RRT_OCC_PER_FACE 4
+struct DOccluder { double n[3], d, en[3][3], eo[3]; };
+struct DShadowProof {
+  DOccluder tri[6][RRT_OCC_PER_FACE];
+  double in_lo[3], in_hi[3];
+  double w[6];            // host: the kept triangles' largest vertex distance from their face
+  uint32_t n[6];
+  uint32_t on, pad;
+};
+
 #define RRT_MAX_QUEUES 8
 #define RRT_QUEUE_STRIDE 16  // counters 64 B apart
 
@@ -172,4 +189,5 @@ struct KParams {
   int32_t* count;
   uint32_t* draws;      // optional
   uint32_t* counters;   // optional [4] per pixel
+  DShadowProof occ;     // last: the hot fields above keep their offsets
 };

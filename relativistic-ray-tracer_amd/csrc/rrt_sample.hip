@@ -45,7 +45,8 @@ __device__ __forceinline__ void park_hit(ShadeLds& cl, uint32_t t, const Isect& 
 
 // estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
-template <bool COUNT, int LEAN, bool NI = false>
+// W: the calling kernel build's tag for the out-of-line occlusion proof (rrt_device.h query_nx)
+template <bool COUNT, int LEAN, bool NI = false, int W = 0>
 __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
@@ -66,7 +67,7 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
       // only the loop state and the RNG stay in registers across the shadow query
       lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
-      if (!query_nx<true, COUNT, NI, LEAN == V_KERR>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
+      if (!query_nx<true, COUNT, NI, LEAN == V_KERR, W>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
         L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
     }
   }
@@ -303,6 +304,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // group leader folds the samples into the pixel sums in sample order (the reference's float /
 // double accumulation order) with the adaptive stop test at every samples_per_batch boundary;
 // samples past the stop are discarded with their draws.  Results equal the sequential loop's.
+// The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light and the
+// general builds (cfg1-3; scenes with environment maps or BSDF sampling); not the point-light
+// build (cfg4: its frame is the camera rays' -- 98% proven misses -- and carrying the proof's code
+// cost it 10%, more than the proof saved) nor the Kerr builds (no planar recurrence).
+#define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 8 * (WAVES) + (LEAN) + 1 : 0)
 #ifndef RRT_BATCH_CALL
 #define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
 #endif
@@ -626,9 +632,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
       else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
-      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
     }
     if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

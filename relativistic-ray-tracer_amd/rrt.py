@@ -25,7 +25,7 @@ RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DI
 RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_PIXEL = 16, 32, 64, 128
 RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED, RRT_RENDER_NO_FIRST = 256, 512, 1024
 RRT_RENDER_ONE_QUEUE, RRT_RENDER_XCD_QUEUES, RRT_RENDER_NO_MISS_PROOF, RRT_RENDER_PREPASS = 2048, 4096, 8192, 16384
-RRT_RENDER_STRIPED_QUEUES = 1 << 15
+RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF = 1 << 15, 1 << 16
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 
@@ -97,7 +97,8 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
-           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks"]
+           "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
+           "rrt_get_occluders"]
 
 _lib = None
 
@@ -135,7 +136,8 @@ def lib():
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
-        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_big_masks", 3)):
+        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_big_masks", 3),
+                             ("rrt_get_occluders", 3)):
             if hasattr(L, name):  # absent from older builds loaded through RRT_LIB
                 getattr(L, name).argtypes = [vp] * n_args
         L.rrt_scene_file_load.argtypes = [C.c_char_p, C.POINTER(vp)]
@@ -161,6 +163,22 @@ def _p(a):
     return None if a is None else a.ctypes.data
 
 
+class ObjectDesc(C.Structure):  # rrt_object_desc
+    _fields_ = [("kind", C.c_uint32), ("bsdf", C.c_uint32), ("n_vertices", C.c_uint32), ("n_triangles", C.c_uint32),
+                ("positions", C.POINTER(C.c_double)), ("normals", C.POINTER(C.c_double)),
+                ("indices", C.POINTER(C.c_uint32)), ("center", C.c_double * 3), ("radius", C.c_double)]
+
+
+class LightDesc(C.Structure):  # rrt_light_desc
+    _fields_ = [("type", C.c_uint32), ("is_delta", C.c_uint32), ("radiance", C.c_float * 3), ("area", C.c_float),
+                ("v", (C.c_double * 3) * 4)]
+
+
+class SceneDesc(C.Structure):  # rrt_scene_desc
+    _fields_ = [("n_objects", C.c_uint32), ("n_bsdfs", C.c_uint32), ("n_lights", C.c_uint32), ("reserved", C.c_uint32),
+                ("objects", C.POINTER(ObjectDesc)), ("bsdfs", C.c_void_p), ("lights", C.POINTER(LightDesc))]
+
+
 class SceneFile:
     """A flattened static scene (.rrts, include/rrt_scene_format.h) loaded by librrt."""
 
@@ -175,6 +193,25 @@ class SceneFile:
 
     def desc(self):
         return lib().rrt_scene_file_desc(self.h)
+
+    def triangles(self):
+        """[n, 3, 3] vertex positions of every mesh triangle, in object / BVH build order."""
+        d = SceneDesc.from_address(self.desc())
+        out = []
+        for i in range(d.n_objects):
+            o = d.objects[i]
+            if o.kind != 0 or o.n_triangles == 0:
+                continue
+            P = np.ctypeslib.as_array(o.positions, shape=(o.n_vertices * 3,)).reshape(-1, 3)
+            idx = np.ctypeslib.as_array(o.indices, shape=(o.n_triangles * 3,)).reshape(-1, 3)
+            out.append(P[idx])
+        return np.concatenate(out) if out else np.zeros((0, 3, 3))
+
+    def lights(self):
+        """[(type, is_delta, v [4][3])] of the scene's lights."""
+        d = SceneDesc.from_address(self.desc())
+        return [(d.lights[i].type, d.lights[i].is_delta, np.array(d.lights[i].v, np.float64))
+                for i in range(d.n_lights)]
 
     def save(self, path):
         rc = lib().rrt_scene_file_save(path.encode(), self.desc())
@@ -381,6 +418,17 @@ class Renderer:
         reach = np.zeros(1, np.float64)
         lib().rrt_get_big_masks(self.h, _p(m), _p(reach))
         return m, float(reach[0])
+
+    def occluders(self):
+        """(tris [6][4][16] = plane n (3), d, in-plane edge normals en [3][3], offsets eo [3];
+        counts [6]) of the shadow-ray occlusion proof's root-box face triangles (include/rrt.h
+        rrt_get_occluders)."""
+        tris = np.zeros((6, 4, 16), np.float64)
+        counts = np.zeros(6, np.uint32)
+        n = lib().rrt_get_occluders(self.h, _p(tris), _p(counts))
+        if n < 0:
+            raise RRTError(n, "no scene")
+        return tris, counts
 
     def clean_tree(self):
         """(boxes [n,6], nodes [n,4] (skip, first, count, ordinal), big_boxes [nb,6], big [nb,3]

@@ -54,13 +54,14 @@ def check(c, rgb, cnt, draws):
 # empty-space grid), the reference-tree walk without the grid, the lane-per-pixel per-sample
 # kernel, the per-pixel-loop kernel and the wavefront state-machine kernel; the sample-parallel
 # kernel also with one chip-wide claim queue, one queue per XCD, and in list order; and the
-# default path with every camera ray marched exactly (no miss proof)
+# default path with every camera ray marched exactly (no miss proof) and with every shadow ray
+# marched exactly (no occlusion proof)
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "xcdqueues": rrt.RRT_RENDER_XCD_QUEUES,
             "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
             "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
-            "wavefront": rrt.RRT_RENDER_WAVEFRONT}
+            "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -74,13 +75,18 @@ def test_small_cases(gpu, name, variant):
     check(c, rgb, cnt, draws)
 
 
-@pytest.mark.parametrize("proof", [True, False])
+PROOFS = {"proofs": 0, "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF,
+          "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
+
+
+@pytest.mark.parametrize("proof", sorted(PROOFS))
 @pytest.mark.parametrize("name", ["cfg1_spheres_480x360_s8", "cfg2_spheres_1080p_s64_flat", "cfg3_bunny_1080p_s64"])
 def test_baseline_frames(gpu, name, proof):
     """The BASELINE.json configs, full frames, bit-exact against the reference (with the
-    camera-ray miss proof, the default, and with every camera ray marched exactly)."""
+    camera-ray miss proof and the shadow-ray occlusion proof, the default, and with either or
+    both rays marched exactly)."""
     c = Case(name)
-    rgb, cnt, draws, _ = render(gpu, c, flags=0 if proof else rrt.RRT_RENDER_NO_MISS_PROOF)
+    rgb, cnt, draws, _ = render(gpu, c, flags=PROOFS[proof])
     check(c, rgb, cnt, draws)
 
 
