@@ -185,6 +185,8 @@ enum {
   RRT_RENDER_NO_MISS_PROOF = 1u << 13, /* march every camera ray exactly instead of first trying
                                      the planar-recurrence miss proof (A/B testing; results
                                      are identical) */
+  RRT_RENDER_NO_PIXEL_PROOF = 1u << 17, /* sample-parallel kernel: no pixel miss proof pass (every
+                                     pixel's camera rays are marched or proven one by one) */
   RRT_RENDER_NO_SHADOW_PROOF = 1u << 16, /* march every shadow ray exactly instead of first trying
                                      the occlusion proof (a certain crossing of a root-box face
                                      triangle before any possible capture; A/B and parity) */

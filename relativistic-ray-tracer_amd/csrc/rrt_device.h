@@ -1030,6 +1030,130 @@ __device__ __forceinline__ bool camera_proven_miss(const KParams& kp, v3 o, v3 d
   return r;
 }
 
+// ------------------------------------------------------------------ pixel miss proof
+// (DESIGN.md §5).  Every camera ray of pixel (px, py) -- jitter anywhere in the pixel's square,
+// part1_code.cpp:182-187 -- is a proven miss.  All the rays start at the camera position O, so
+// they share x = (O - c) / |O - c| and u = 1 / |O - c|; a ray's planar march depends on its
+// direction only through dx = d . x (u' = -u dx / sqrt(1 - dx^2)), and its plane only through
+// y.  The proof runs the recurrence for the pixel's least, central and largest dx (from its
+// corners and centre, widened for curvature) and, while the three agree in the sign of every v
+// and vary little, bounds every ray's points around the central ray's: with the frame (ea, eb)
+// the same for all, |P - P_c| <= rho |1/v - 1/v_c| + (rho / |v|) |eb| |y - y_c|.  Each segment
+// of the central ray must then clear the root box by the camera proof's margin plus that bound.
+// Launch constants are the camera proof's (KParams::miss) and the camera's.
+__device__ __forceinline__ v3 pixel_ray_dir(const KParams& kp, double sx, double sy) {
+  const DCamera& cam = kp.cam;
+  const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
+  const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+  const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+  return unit(w);
+}
+__device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px, uint32_t py) {
+#pragma clang fp contract(fast)
+  const DMissProof& mp = kp.miss;
+  const DHole& h = kp.hole;
+  const v3 O = ld3(kp.cam.pos), c = ld3(h.c);
+  const v3 x0 = O - c;
+  const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
+  const v3 X = vmul(x0, u0);
+  // the pixel's directions: dx range, the centre's plane axis y_c and the spread of y
+  const v3 dc = pixel_ray_dir(kp, px + 0.5, py + 0.5);
+  const double dxc = dot(dc, X);
+  v3 Yc = dc - smul(dxc, X);
+  const double dyc = sqrt(norm2(Yc));
+  if (!(dyc > 1e-3)) return false;  // towards the hole: no stable plane
+  Yc = vmul(Yc, 1.0 / dyc);
+  double dlo = dxc, dhi = dxc, dY = 0.0, dd = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const v3 d = pixel_ray_dir(kp, (double)px + (k & 1), (double)py + (k >> 1));
+    const double dx = dot(d, X);
+    dlo = fmin(dlo, dx);
+    dhi = fmax(dhi, dx);
+    const v3 yv = d - smul(dx, X);
+    const double dy = sqrt(norm2(yv));
+    if (!(dy > 1e-3)) return false;
+    dY = fmax(dY, sqrt(norm2(vmul(yv, 1.0 / dy) - Yc)));
+    dd = fmax(dd, sqrt(norm2(d - dc)));
+  }
+  // a smooth function over the small square: extremes within the corners' values plus a
+  // curvature term of the square's angular radius squared
+  const double slack = 2.0 * dd * dd + 1e-12, wdx = dhi - dlo;
+  dlo -= 0.05 * wdx + slack;
+  dhi += 0.05 * wdx + slack;
+  dY = 1.25 * dY + slack;
+  if (!(dlo > -1.0 && dhi < 1.0)) return false;
+  // three planar recurrences (least, central, largest dx), started at A = O as the shadow proof
+  double s[3], vp[3];
+  {
+    const double dxs[3] = {dlo, dxc, dhi};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double up0 = -u0 * dxs[i] / sqrt(1.0 - dxs[i] * dxs[i]);
+      vp[i] = mp.rho * u0;
+      s[i] = u0 * mp.co1 - up0 * h.sin_dt * mp.inv_rho;
+    }
+  }
+  double ea = 1.0, eb = 0.0, sig = 1.0, rp = r0, dpa = 0.0, dvp = 0.0;  // A = O: the same for all rays
+  const double si2 = h.sin_dt * h.sin_dt;
+#pragma unroll 1
+  for (int j = 0; j < h.steps; ++j) {
+    double v[3];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double up = (vp[i] * mp.co1 - mp.rho * s[i]) * mp.inv_si;
+      s[i] = fabs(vp[i]) * mp.inv_rho;
+      const double f1 = -s[i] + mp.k15 * s[i] * s[i];
+      const double u2 = s[i] + up * (h.dt * 0.5);
+      const double f2 = -u2 + mp.k15 * u2 * u2;
+      const double u3 = u2 + f1 * mp.dt2_4;
+      const double f3 = -u3 + mp.k15 * u3 * u3;
+      v[i] = s[i] + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
+      ok = ok && fabs(v[i]) >= mp.kappa * (s[i] + fabs(up) * h.dt);  // NaN: false
+    }
+    // one sign history for the whole pixel, and v far from 0 compared with its spread
+    const double dv = 1.5 * fmax(fabs(v[0] - v[1]), fabs(v[2] - v[1]));
+    const double av = fabs(v[1]);
+    if (!(ok && (v[0] < 0.0) == (v[1] < 0.0) && (v[2] < 0.0) == (v[1] < 0.0) && av > 2.0 * dv)) return false;
+    const double sg = vp[1] < 0.0 ? -1.0 : 1.0;
+    const double a = sg * mp.co1, b = sig * mp.si1;
+    const double na = a * ea - b * eb, nb = a * eb + b * ea;
+    sig *= sg;
+    const double r = mp.rho / (av - dv) * (1.0 + 1e-6);  // |B - c| over the pixel (upper bound)
+    const double dpb = mp.rho * dv / (av * (av - dv)) * (1.0 + 1e-6) + r * fabs(nb) * dY;
+    const double m0 = mp.eta * (fmax(rp, r) + mp.scale);
+    const double m = m0 + fmax(dpa, dpb);
+    // Distance from the hole: a ray's segment depends only on its (v_prev, v) -- turning the
+    // plane about x keeps it -- and the pixel's pairs lie in [v_prev +- dvp] x [v +- dv]; the
+    // camera proof's scalar test must hold at the four corners of that box.  D is convex there
+    // (its maximum, the nearest line, at a corner) and |v|, |v_prev| are largest at corners.
+    const double rb = mp.r_ball + m0;
+    bool far = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double w = v[1] + ((k & 1) ? dv : -dv), wp = vp[1] + ((k & 2) ? dvp : -dvp);
+      const double aw = fabs(w), awp = fabs(wp);
+      const double D = w * w + wp * wp - 2.0 * mp.co1 * awp * w;
+      const bool inside = w * (mp.co1 * awp - w) < 0.0 && awp * (awp - mp.co1 * w) > 0.0;
+      far = far && (inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(w * w, wp * wp));
+      (void)aw;
+    }
+    if (!far) {
+      const double ia = mp.rho / vp[1], ib = mp.rho / v[1];
+      const v3 pa = j == 0 ? O : V(c.x + (ea * ia) * X.x + (eb * ia) * Yc.x, c.y + (ea * ia) * X.y + (eb * ia) * Yc.y,
+                                   c.z + (ea * ia) * X.z + (eb * ia) * Yc.z);
+      const v3 pb = V(c.x + (na * ib) * X.x + (nb * ib) * Yc.x, c.y + (na * ib) * X.y + (nb * ib) * Yc.y,
+                      c.z + (na * ib) * X.z + (nb * ib) * Yc.z);
+      if (!seg_clear_of_box(pa, pb, mp.lo, mp.hi, m)) return false;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vp[i] = v[i];
+    rp = r; dpa = dpb; dvp = dv; ea = na; eb = nb;
+  }
+  return true;
+}
+
 // query() behind a call: the caller keeps only what is live across the call, the walk gets the
 // register file to itself (rrt_sample.hip batch kernel)
 template <bool ANY, bool KERR>

@@ -27,6 +27,7 @@ hipError_t rrt_launch_mega(const KParams& kp, const KParams* d_kp, int count, in
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -35,7 +36,7 @@ hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float
 namespace {
 
 constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
-constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;  // claim counters
+constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);  // claim counters + the pixel proof's list length
 
 struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
@@ -145,6 +146,8 @@ struct rrt_ctx {
   size_t order_cap = 0;
   std::vector<uint32_t> h_order;  // what d_order holds
   KParams::FirstSample* d_first = nullptr;  // batch kernel: sample 0 per pixel slot
+  uint32_t* d_list = nullptr;  // batch kernel: the pixel proof's claim list
+  size_t list_cap = 0;
   size_t first_cap = 0;
   float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
   size_t px_cap = 0;
@@ -218,7 +221,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipSetDevice(c->device);
     free_scene_dev(c);
     free_env_dev(c);
-    hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
+    hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_list); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -1177,6 +1180,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
     kp.tile_order = c->d_order;
     kp.first = nullptr;
+    kp.claim_list = nullptr; kp.claim_count = nullptr;
     // sample-0 pre-pass: off by default (with the slot speculation a wrong first hypothesis
     // costs one round, less than the extra pass; tools/ab_kernels.py cfg3 46.4 vs 47.8 ms)
     if ((p->flags & RRT_RENDER_PREPASS) && !(p->flags & RRT_RENDER_NO_FIRST)) {
@@ -1186,6 +1190,18 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         c->first_cap = kp.n_pixels;
       }
       kp.first = c->d_first;
+    }
+    // pixel miss proof pass (rrt_pixel_proof_kernel): the area/point-light builds, whose misses
+    // are black, with a claim order it can compact (striped or one queue)
+    if ((lean == 1 || lean == 2) && kp.miss.on && !c->env_w && !kp.first && (striped || nq == 1) &&
+        !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
+      if (c->list_cap < kp.n_pixels) {
+        hipFree(c->d_list); c->d_list = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_list, sizeof(uint32_t) * kp.n_pixels));
+        c->list_cap = kp.n_pixels;
+      }
+      kp.claim_list = c->d_list;
+      kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
     }
   }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
@@ -1206,10 +1222,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     const uint32_t fwv = (p->variant >> 8) & 0xfu;  // pre-pass waves/SIMD (A/B), default 3
     const int fw = (lean == 1 && (fwv == 4 || fwv == 5)) ? (int)fwv : 3;
     if (kp.first) std::snprintf(first, sizeof(first), "rrt_first_kernel<%d, %d> + ", lean, fw);
+    if (kp.claim_list) std::snprintf(first, sizeof(first), "rrt_pixel_proof_kernel + ");
     std::snprintf(name, sizeof(name), "%srrt_batch_kernel<%d, %d>", first, lean, w);
     if (kp.first)
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, fw, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
+    if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
   } else if (mega) {
     std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);

@@ -178,6 +178,10 @@ struct KParams {
   uint32_t n_queues;
   uint32_t q_end[RRT_MAX_QUEUES];
   uint32_t q_stripe;     // 1: queue q holds claims q, q + n_queues, ... of the whole order (q_end unused)
+  // pixel miss proof (rrt_pixel_proof_kernel): the claim indices whose pixels were not proven
+  // all-miss, in claim order per wave, and their count; null: every pixel is claimed
+  uint32_t* claim_list;
+  uint32_t* claim_count;
   struct FirstSample { float r, g, b; uint32_t hit; };
   FirstSample* first;          // sample 0 of every pixel slot (rrt_first_kernel), or null
   uint32_t group;        // lanes per pixel (power of two, 2..32)

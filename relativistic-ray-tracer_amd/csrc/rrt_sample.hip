@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
+
   uint64_t t_claim = 0;  // when the group claimed its pixel (wall clock)
 
   for (;;) {
@@ -376,8 +377,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     // consecutive claims as there are leaders (2 with the BASELINE group size), lane 0 issues it.
     const uint64_t needers = __ballot(gl == 0 && !have && !done);
     if (needers) {
+      // claim space: every pixel slot, or the pixel proof's list padded to whole stripes (the
+      // padding claims no pixel); read here, not held through the kernel
+      const uint32_t n_list = kp.claim_list ? *kp.claim_count : 0u;
+      const uint32_t npx = kp.claim_list ? (n_list + RRT_STRIPE - 1) / RRT_STRIPE * RRT_STRIPE : kp.n_pixels;
       uint64_t pending = needers;
-      uint32_t p = kp.n_pixels + 1;  // n_pixels + 1: this group did not claim
+      uint32_t p = npx + 1;  // npx + 1: this group did not claim
       while (pending) {
         const uint32_t want = (uint32_t)__popcll(pending);
         uint32_t base = 0, got = 0, out = 0, qc = 0;
@@ -389,8 +394,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
             // consecutive claims (n_pixels is a multiple of 64: tiles of 8k x 8k pixels)
             const uint32_t nq = kp.n_queues;
             const uint32_t qb = kp.q_stripe ? 0u : (q ? kp.q_end[q - 1] : 0u);
-            const uint32_t qn = kp.q_stripe ? (kp.n_pixels / RRT_STRIPE - q + nq - 1) / nq * RRT_STRIPE
-                                            : kp.q_end[q] - qb;
+            const uint32_t qn = kp.q_stripe ? (npx / RRT_STRIPE - q + nq - 1) / nq * RRT_STRIPE
+                                            : (kp.claim_list ? npx : kp.q_end[q] - qb);
             const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, want);
             if (k < qn) {
               base = qb + k; got = min(want, qn - k); qc = q;
@@ -408,15 +413,15 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
           const uint32_t ix = base + rank;
           p = kp.q_stripe ? ((ix / RRT_STRIPE) * kp.n_queues + qc) * RRT_STRIPE + ix % RRT_STRIPE : ix;
         }
-        if (mine && out) p = kp.n_pixels;
+        if (mine && out) p = npx;
         pending = out ? 0ull : (got >= want ? 0ull : pending & ~__ballot(gl == 0 && mine && rank < got));
       }
       q = __shfl(q, 0);
       q_left = __shfl(q_left, 0);
       p = __shfl(p, (int)gbase);
-      if (p == kp.n_pixels + 1) {
+      if (p == npx + 1) {
         // (the group kept its pixel)
-      } else if (p >= kp.n_pixels) {
+      } else if (p >= npx) {
         done = true;
 #if RRT_PROFILE
         if (gl == 0) atomicMin(&rrt_prof[11], (unsigned long long)wall_clock64());
@@ -425,9 +430,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 #if RRT_PROFILE
         ++prof_blocks;
 #endif
-        const uint32_t tl = kp.tile_order[p / tpix], r = p % tpix, lx = r % ts, ly = r / ts;
+        const uint32_t ix = kp.claim_list ? (p < n_list ? kp.claim_list[p] : kp.n_pixels) : p;
+        const uint32_t pi = ix < kp.n_pixels ? ix : 0u;
+        const uint32_t tl = kp.tile_order[pi / tpix], r = pi % tpix, lx = r % ts, ly = r / ts;
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
-        if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
+        if (ix < kp.n_pixels && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
           if (gl == 0) {
             const uint32_t slot = tl * tpix + r;
             lput(gs.px, gid, x); lput(gs.py, gid, y); lput(gs.slot, gid, slot);
@@ -723,6 +730,43 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     rrt_prof_work[w] = ((unsigned long long)nb << 32) | prof_samples;
   }
 #endif
+}
+
+// Pixel miss proof pass (rrt_device.h pixel_miss_proof), one lane per claim index
+// in the batch kernel's order: a pixel whose every camera ray is a proven miss renders to black
+// (no environment map in these builds): its samples are all zero, so it stops at the first
+// adaptive check (raytrace_pixel, part1_code.cpp:147-158) with count = min(ns_aa,
+// samples_per_batch) and count * draws_miss draws -- written here.  The others go to the claim
+// list, appended per wave (one atomic) so claims keep their order within each wave's run.
+__global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
+  using namespace rrt;
+  const uint32_t ix = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  bool listed = false;
+  if (ix < kp.n_pixels) {
+    const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+    const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
+    if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
+      if (pixel_miss_proof(kp, x, y)) {
+        const uint32_t slot = tl * tpix + r, n = min(kp.ns_aa, kp.samples_per_batch);
+        kp.rgb[3 * slot] = 0.0f; kp.rgb[3 * slot + 1] = 0.0f; kp.rgb[3 * slot + 2] = 0.0f;
+        kp.count[slot] = (int32_t)n;
+        if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
+      } else {
+        listed = true;
+      }
+    }
+  }
+  const uint64_t b = __ballot(listed);
+  uint32_t base = 0;
+  if (lane == 0 && b) base = atomicAdd(kp.claim_count, (uint32_t)__popcll(b));
+  base = __shfl(base, 0);
+  if (listed) kp.claim_list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = ix;
+}
+hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream) {
+  hipLaunchKernelGGL(rrt_pixel_proof_kernel, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_kp);
+  return hipGetLastError();
 }
 
 // Sample 0 of every pixel, one lane per pixel (tile-list order, so a wave covers two rows of a

@@ -25,7 +25,7 @@ RRT_RENDER_COUNTERS, RRT_RENDER_DRAWS, RRT_RENDER_WAVEFRONT, RRT_RENDER_EXACT_DI
 RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_PIXEL = 16, 32, 64, 128
 RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED, RRT_RENDER_NO_FIRST = 256, 512, 1024
 RRT_RENDER_ONE_QUEUE, RRT_RENDER_XCD_QUEUES, RRT_RENDER_NO_MISS_PROOF, RRT_RENDER_PREPASS = 2048, 4096, 8192, 16384
-RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF = 1 << 15, 1 << 16
+RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF, RRT_RENDER_NO_PIXEL_PROOF = 1 << 15, 1 << 16, 1 << 17
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 

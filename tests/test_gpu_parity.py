@@ -61,7 +61,8 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
             "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
             "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
-            "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
+            "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
+            "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -75,8 +76,10 @@ def test_small_cases(gpu, name, variant):
     check(c, rgb, cnt, draws)
 
 
-PROOFS = {"proofs": 0, "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF,
-          "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
+PROOFS = {"proofs": 0,
+          "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF | rrt.RRT_RENDER_NO_PIXEL_PROOF,
+          "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
+          "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF}
 
 
 @pytest.mark.parametrize("proof", sorted(PROOFS))

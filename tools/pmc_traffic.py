@@ -16,7 +16,7 @@ def kernel_values(d, counter):
         k = r["Kernel_Name"]
         if r["Counter_Name"] != counter or not k.startswith("void rrt_"):
             continue
-        if not any(s in k for s in ("batch", "first", "sample", "render_kernel", "mega")):
+        if not any(s in k for s in ("batch", "first", "pixel_proof", "sample", "render_kernel", "mega")):
             continue
         name = k[len("void "):].split("(")[0]
         did = int(r["Dispatch_Id"])
@@ -35,8 +35,8 @@ def main():
     fetch, write = kernel_values(a.fetch, "FETCH_SIZE"), kernel_values(a.write, "WRITE_SIZE")
     if not fetch:
         raise SystemExit("no render-kernel dispatch in the PMC output")
-    # one render launch = the sample-0 pre-pass (if any) + the main kernel
-    names = sorted(fetch, key=lambda n: (0 if n.startswith("rrt_first") else 1, n))
+    # one render launch = the pre-pass (pixel miss proof or sample 0, if any) + the main kernel
+    names = sorted(fetch, key=lambda n: (0 if n.startswith(("rrt_first", "rrt_pixel_proof")) else 1, n))
     fkb = sum(fetch[n] for n in names)
     wkb = sum(write.get(n, 0.0) for n in names)
     out = {"workload": a.workload, "kernel": " + ".join(names), "fetch_size_kb": fkb, "write_size_kb": wkb,
