@@ -73,11 +73,11 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl
   }
   return L / (float)total;
 }
-template <bool COUNT, int LEAN>
+template <bool COUNT, int LEAN, int W = 0>
 __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
-  return direct_importance_parked<COUNT, LEAN>(kp, g, cl, t, cn);
+  return direct_importance_parked<COUNT, LEAN, false, W>(kp, g, cl, t, cn);
 }
 
 // estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
@@ -108,6 +108,14 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 }
 
 }  // namespace rrt
+
+// The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light and the
+// general builds (cfg1-3; scenes with environment maps or BSDF sampling); not the point-light
+// build (cfg4: its frame is the camera rays' -- 98% proven misses -- and carrying the proof's code
+// cost it 10%, more than the proof saved) nor the Kerr builds (no planar recurrence).  One tag per
+// kernel build (batch kernels; per-sample kernels, counting or not).
+#define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 8 * (WAVES) + (LEAN) + 1 : 0)
+#define RRT_OCC_TAG_S(COUNT, LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 64 + ((COUNT) ? 128 : 0) + 8 * (WAVES) + (LEAN) + 1 : 0)
 
 #if RRT_PROFILE
 // [0..7] per-phase wave cycles (busiest lane per wave, summed): total, camera queries, micro
@@ -230,9 +238,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
           query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
-        else if (is_lean(LEAN)) s = e + direct_importance_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
+        else if (is_lean(LEAN)) s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
         else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
-        else s = e + direct_importance_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
+        else s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
       } else if (!is_lean(LEAN) && kp.env.w) {
         s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
       }
@@ -304,11 +312,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // group leader folds the samples into the pixel sums in sample order (the reference's float /
 // double accumulation order) with the adaptive stop test at every samples_per_batch boundary;
 // samples past the stop are discarded with their draws.  Results equal the sequential loop's.
-// The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light and the
-// general builds (cfg1-3; scenes with environment maps or BSDF sampling); not the point-light
-// build (cfg4: its frame is the camera rays' -- 98% proven misses -- and carrying the proof's code
-// cost it 10%, more than the proof saved) nor the Kerr builds (no planar recurrence).
-#define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 8 * (WAVES) + (LEAN) + 1 : 0)
 #ifndef RRT_BATCH_CALL
 #define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
 #endif

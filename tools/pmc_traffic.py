@@ -14,11 +14,13 @@ def kernel_values(d, counter):
     vals = {}
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if r["Counter_Name"] != counter or not k.startswith("void rrt_"):
+        if k.startswith("void "):
+            k = k[len("void "):]
+        if r["Counter_Name"] != counter or not k.startswith("rrt_"):
             continue
         if not any(s in k for s in ("batch", "first", "pixel_proof", "sample", "render_kernel", "mega")):
             continue
-        name = k[len("void "):].split("(")[0]
+        name = k.split("(")[0]
         did = int(r["Dispatch_Id"])
         vals.setdefault(name, {}).setdefault(did, 0.0)
         vals[name][did] += float(r["Counter_Value"])
