@@ -50,7 +50,8 @@ def main():
             print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
     same = len(set(s for v, s in sums.items() if ":" not in v)) <= 1  # diagnostic flags change outputs
     print(json.dumps({"workload": a.workload, "identical_outputs": same,
-                      "median_ms": {v: float(np.median(t)) for v, t in times.items()}}))
+                      "median_ms": {v: float(np.median(t)) for v, t in times.items()},
+                      "sums": {v: list(x) for v, x in sums.items()}}))
 
 
 if __name__ == "__main__":

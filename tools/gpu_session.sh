@@ -47,6 +47,7 @@ for step in "$@"; do
     cache) run pmc_lat 600 rocprofv3 --pmc TCP_TCP_LATENCY_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --kernel-trace -d gpurun_out/pmc_lat -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0} ;;
+    kerr)  run pytest_kerr 600 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 300 --timeout-method thread ;;
     abw)   run abw 900 python3 tools/ab_workload.py --workload ${AB_WORKLOAD:-cfg5} --rounds ${AB_ROUNDS:-2} ${AB_WVARIANTS:-0 0:2048} ;;
     prof5) run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline ;;
     diag)  run diag 600 python3 tools/diag_clear.py --res 64 128 192 256 ;;
