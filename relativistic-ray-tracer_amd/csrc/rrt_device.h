@@ -884,51 +884,6 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
   return false;
 }
 
-// The Kerr counterpart (DESIGN.md §10 "Occlusion proof").  The Kerr march has no planar
-// recurrence, but its segment chain is cheap next to the walks: this marches the exact chain of
-// query_kerr (the same steps, IEEE fallback included, so the same end points bit for bit) without
-// walking the BVH, and accepts "occluded" when a segment that leaves the trigger box certainly
-// crosses a wall triangle (occ_exit, margin m for the walk's own rounding of the segment) before
-// any capture or escape.  query_kerr's walk of that segment (or of an earlier one) then hits, so
-// the shadow query returns true.  A capture, an escape, the end of the sweep or a segment leaving
-// the root box without a certain crossing is no proof: the caller marches with the walks.
-template <int W = 0>
-__device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d) {
-  const DHole& h = kp.hole;
-  const DShadowProof& sp = kp.occ;
-  const double m = kp.miss.eta * (kp.miss.r_ball + kp.miss.scale);
-  v3 q, p;
-  kerr_init(h, o, d, q, p);
-  v3 a = o;
-  bool a_in = occ_inside(sp, o);
-  const double rh2 = h.r_hor * h.r_hor;
-  double swept = 0.0;
-#pragma unroll 1
-  for (int j = 0; j < h.kerr_max_steps && swept < 2.0 * PI_D; ++j) {
-    v3 q1 = q, p1 = p;
-    double sw1 = swept;
-    KArith<!RRT_LIBM_DIVSQRT> fast;
-    bool escaped = kerr_advance(h, q1, p1, sw1, fast);
-    if (__builtin_expect(!fast.ok, 0)) {
-      KArith<false> ieee;
-      q1 = q; p1 = p; sw1 = swept;
-      escaped = kerr_advance(h, q1, p1, sw1, ieee);
-    }
-    if (escaped) return false;
-    q = q1; p = p1; swept = sw1;
-    if (kerr_r2(h, q) <= rh2) return false;  // captured first: no proof
-    const v3 b = kerr_world(h, q);
-    const bool b_in = occ_inside(sp, b);
-    if (!b_in || !a_in) {
-      const int res = occ_exit_call<W>(kp, a, b, m);
-      if (res) return res > 0;
-    }
-    a_in = b_in;
-    a = b;
-  }
-  return false;
-}
-
 // BVHAccel::intersect (bvh.cpp:103-113): march the geodesic as straight micro segments; the
 // incoming ray's min_t / max_t are dropped (camera clip planes and shadow-ray distance are
 // ignored, as in the reference).  Capture by the hole returns "no hit".  KERR: the Kerr build
@@ -1219,12 +1174,11 @@ __device__ __noinline__ bool shadow_proof_call(const KParams& kp, v3 o, v3 d) {
 // W: the occlusion proof's build tag (0: none)
 template <bool ANY, bool COUNT, bool NI, bool KERR = false, int W = 0>
 __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  // shadow rays: the occlusion proof first (never in the reference-work counts)
-  if (RRT_SHADOW_PROOF && W && ANY && kp.occ.on && !(COUNT && !kp.count_exec)) {
+  // shadow rays: the occlusion proof first (Schwarzschild; never in the reference-work counts)
+  if (RRT_SHADOW_PROOF && W && ANY && !KERR && kp.occ.on && !(COUNT && !kp.count_exec)) {
     RRT_T0(tp0);
-    const bool occluded = KERR ? kerr_occluded_proof<W>(kp, o, d)
-                          : RRT_SHADOW_MODE == 1 ? shadow_proof_call<W>(kp, o, d)
-                                                 : shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
+    const bool occluded = RRT_SHADOW_MODE == 1 ? shadow_proof_call<W>(kp, o, d)
+                                               : shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
     RRT_ACC(t_squery, tp0);
     if (occluded) return true;
   }

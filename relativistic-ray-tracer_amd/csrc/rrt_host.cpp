@@ -1063,11 +1063,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       kp.occ.in_hi[k] = kp.miss.hi[k] - kp.occ.w[k + 3] - m2;
     }
     // the point-light scenes' builds carry no proof (rrt_sample.hip RRT_OCC_TAG); off for them in
-    // every kernel, so the counting passes count what their batch kernel executes.  The Kerr
-    // builds carry the exact-march proof (rrt_device.h kerr_occluded_proof) whatever the lights.
-    const bool kerr_sp = c->hole.kind == RRT_METRIC_KERR;
-    const bool metric_ok = kerr_sp ? (c->hole.dt > 0.0 && std::isfinite(c->hole.dt)) : (kp.miss.on && c->lean != 2);
-    kp.occ.on = (metric_ok && any && fin && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
+    // every kernel, so the counting passes count what their batch kernel executes
+    kp.occ.on = (kp.miss.on && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
   }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;

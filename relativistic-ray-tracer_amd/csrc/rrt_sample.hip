@@ -109,13 +109,13 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 
 }  // namespace rrt
 
-// The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light, the
-// general and the Kerr builds (cfg1-3, cfg5; the Kerr builds take kerr_occluded_proof); not the
-// point-light build (cfg4: its frame is the camera rays' -- 98% proven misses -- and carrying the
-// proof's code cost it 10%, more than the proof saved).  One tag per kernel build (batch kernels;
-// per-sample kernels, counting or not).
-#define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) != 2 ? 8 * (WAVES) + (LEAN) + 1 : 0)
-#define RRT_OCC_TAG_S(COUNT, LEAN, WAVES) ((LEAN) != 2 ? 64 + ((COUNT) ? 128 : 0) + 8 * (WAVES) + (LEAN) + 1 : 0)
+// The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light and the
+// general builds (cfg1-3; scenes with environment maps or BSDF sampling); not the point-light
+// build (cfg4: its frame is the camera rays' -- 98% proven misses -- and carrying the proof's code
+// cost it 10%, more than the proof saved) nor the Kerr builds (no planar recurrence).  One tag per
+// kernel build (batch kernels; per-sample kernels, counting or not).
+#define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 8 * (WAVES) + (LEAN) + 1 : 0)
+#define RRT_OCC_TAG_S(COUNT, LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 64 + ((COUNT) ? 128 : 0) + 8 * (WAVES) + (LEAN) + 1 : 0)
 
 #if RRT_PROFILE
 // [0..7] per-phase wave cycles (busiest lane per wave, summed): total, camera queries, micro

@@ -29,7 +29,7 @@ KERR_CASES = [
 ]
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
-            "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
+            "onequeue": rrt.RRT_RENDER_ONE_QUEUE}
 _oracle_cache = {}
 
 

@@ -123,72 +123,3 @@ def test_occluded_rays_really_hit_before_capture(name, min_share, lead):
         assert O.lib().ro_tri_intersect(T[tri[i]].ravel().copy(), zero_n, rows[i, k, 0:3].copy(),
                                         rows[i, k, 3:6].copy(), C.byref(mt), hit_p, nrm) == 1, (name, i, k)
     assert proven.mean() >= min_share
-
-
-KERR_CASES = [("cfg3_bunny_1080p_s64", 0.9, (0.0, 1.0, 0.0), 0.5), ("cfg1_spheres_480x360_s8", 0.6, (0.3, 1.0, -0.2), 0.4)]
-
-
-def kerr_proof(chain, frame, c, faces, box, K, m, max_steps):
-    """rrt_device.h kerr_occluded_proof over the restatement's exact chain of one ray: (proven,
-    segment index, triangle index).  The sweep / escape ends only shorten the kernel's march."""
-    ex, ey, ez = frame
-    a = chain[0, 0:3]
-    a_in = _inside_box(box, a)
-    for j in range(min(len(chain), max_steps)):
-        if chain[j, 7]:
-            return False, j, -1  # captured first
-        q = chain[j, 8:11]
-        b = np.array([c[k] + ((ex[k] * q[0] + ey[k] * q[1]) + ez[k] * q[2]) for k in range(3)])
-        b_in = _inside_box(box, b)
-        if not (b_in and a_in):
-            res, idx = _exit_k(faces, box, K, a, b, m)
-            if res:
-                return res > 0, j, idx
-        a_in, a = b_in, b
-    return False, -1, -1
-
-
-def _inside_box(box, p):
-    return bool(np.all(p >= box[0]) and np.all(p <= box[1]))
-
-
-def _exit_k(faces, box, K, a, b, m):
-    from shadow_proof_sim import _exit
-    return _exit(faces, box, K, a, b, m)
-
-
-@pytest.mark.parametrize("name,spin,axis,min_share", KERR_CASES)
-def test_kerr_occluded_rays_really_hit_before_capture(name, spin, axis, min_share):
-    """The Kerr occlusion proof (exact march, no walks; rrt_device.h kerr_occluded_proof) on shadow
-    rays towards the area lights and in uniform directions (the environment light's): every proven
-    ray is not captured up to the proof's segment, and the restatement's triangle test accepts that
-    exact segment against the proof's triangle -- so the Kerr shadow query returns true."""
-    from miss_proof_sim import ETA
-    c, sf, lo, hi, _, _ = _setup(name)
-    T = sf.triangles()
-    faces, w = occluders(T, lo, hi)
-    bh = np.array(c.cfg["bh"], np.float64)
-    K = constants(bh, lo, hi)
-    box = trigger_box(K, w)
-    m = ETA * (K["r_ball"] + K["scale"])
-    n = 600
-    o, d = _shadow_rays(T, sf.lights(), n, 12)
-    g = np.random.default_rng(13)
-    u = g.normal(size=(n, 3))
-    u /= np.linalg.norm(u, axis=1)[:, None]
-    o = np.concatenate([o, o + EPS * (u - d)])
-    d = np.concatenate([d, u])
-    hit_p, nrm, zero_n = np.zeros(3), np.zeros(3), np.zeros(9)
-    proven = 0
-    for i in range(len(o)):
-        chain, frame = O.kerr_chain(bh, spin, axis, o[i], d[i], max_rows=4 * K["steps"])
-        ok, k, tri = kerr_proof(chain, frame, bh[:3], faces, box, K, m, 4 * K["steps"])
-        if not ok:
-            continue
-        proven += 1
-        assert not chain[:k + 1, 7].any(), (name, i, k)
-        mt = C.c_double(chain[k, 6])
-        assert O.lib().ro_tri_intersect(T[tri].ravel().copy(), zero_n, chain[k, 0:3].copy(), chain[k, 3:6].copy(),
-                                        C.byref(mt), hit_p, nrm) == 1, (name, i, k)
-    print(name, spin, "proven share", proven / len(o))
-    assert proven / len(o) >= min_share
