@@ -161,6 +161,9 @@ __device__ __forceinline__ bool in_fast_range(double v) {
   const double a = fabs(v);
   return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
 }
+#ifndef RRT_WALK_PREFETCH
+#define RRT_WALK_PREFETCH 0  // 1: traverse_clean prefetches both successor nodes (A/B)
+#endif
 #ifndef RRT_SLAB_APPROX
 #define RRT_SLAB_APPROX 1  // 0: every fast slab test takes the Markstein quotients (A/B)
 #endif
@@ -410,6 +413,16 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
     const DNode* n = more ? &kp.clean_nodes[node] : nullptr;
     const bool big = next_big < (more ? n->pad : 0x7fffffff);
     if (!big && !more) break;
+#if RRT_WALK_PREFETCH
+    // warm the cache lines of both possible next nodes (node + 1, the left child, after a passing
+    // inner box; skip otherwise) while this box is tested: the walk is a chain of dependent node
+    // loads.  The values are consumed only at the end of the iteration.
+    uint32_t w0 = 0u, w1 = 0u;
+    if (more && !big) {
+      if (n->count == 0) w0 = *(const volatile uint32_t*)&kp.clean_nodes[node + 1];
+      if (n->skip >= 0) w1 = *(const volatile uint32_t*)&kp.clean_nodes[n->skip];
+    }
+#endif
     const double* mn = big ? kp.big[bi].mn : n->mn;
     const double* mx = big ? kp.big[bi].mx : n->mx;
     const int first = big ? kp.big[bi].first : n->first;
@@ -425,6 +438,9 @@ __device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3
       hit = true;
       if (ANY) return true;
     }
+#if RRT_WALK_PREFETCH
+    asm volatile("" ::"v"(w0), "v"(w1));
+#endif
     if (big) {
       bi = next_big_in(bmask, bi + 1, nb);
       next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;

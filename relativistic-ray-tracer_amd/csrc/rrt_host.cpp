@@ -1194,9 +1194,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       kp.first = c->d_first;
     }
     // pixel miss proof pass (rrt_pixel_proof_kernel): the area/point-light builds, whose misses
-    // are black, with a claim order it can compact (striped or one queue)
+    // are black, with a claim order it can compact (striped or one queue); list entries keep bit
+    // 31 for the first-hypothesis hint
     if ((lean == 1 || lean == 2) && kp.miss.on && !c->env_w && !kp.first && (striped || nq == 1) &&
-        !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
+        kp.n_pixels < 0x80000000u && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
       if (c->list_cap < kp.n_pixels) {
         hipFree(c->d_list); c->d_list = nullptr;
         HIPCHK(c, hipMalloc(&c->d_list, sizeof(uint32_t) * kp.n_pixels));

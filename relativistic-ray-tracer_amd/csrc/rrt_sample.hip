@@ -321,6 +321,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 template <int LEAN>
 struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
 #define RRT_STRIPE 16  // striped claim queues: runs of consecutive claims (neighbouring pixels)
+#ifndef RRT_CLAIM_HYP
+#define RRT_CLAIM_HYP 1  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
+                         // proof pass's hint (A/B: cfg3 23.9 / 22.7 ms for 0 / 1)
+#endif
 #ifndef RRT_TAIL_PRIO
 #define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
 #endif
@@ -433,7 +437,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 #if RRT_PROFILE
         ++prof_blocks;
 #endif
-        const uint32_t ix = kp.claim_list ? (p < n_list ? kp.claim_list[p] : kp.n_pixels) : p;
+        // a list entry: pixel claim index | hint << 31 (rrt_pixel_proof_kernel)
+        const uint32_t ent = kp.claim_list ? (p < n_list ? kp.claim_list[p] : kp.n_pixels) : p;
+        const uint32_t ix = kp.claim_list ? (ent & 0x7fffffffu) : ent;
         const uint32_t pi = ix < kp.n_pixels ? ix : 0u;
         const uint32_t tl = kp.tile_order[pi / tpix], r = pi % tpix, lx = r % ts, ly = r / ts;
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
@@ -452,7 +458,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
               lput(gs.i, gid, 1u); lput(gs.O, gid, f0.hit ? Dh : Dm); lput(gs.hyp, gid, f0.hit);
             } else {
               lput(gs.O, gid, 0u); lput(gs.i, gid, 0u);
-              lput(gs.hyp, gid, 0u);  // speculate "miss"
+              // The first step's hypothesis: "miss" without the pixel proof's list; for a listed
+              // pixel (one whose camera rays are not all proven misses) RRT_CLAIM_HYP 1 takes
+              // "hit", 2 the list entry's hint (its central ray is no proven miss)
+              const uint32_t hyp0 = !kp.claim_list ? 0u : RRT_CLAIM_HYP == 2 ? (ent >> 31) : RRT_CLAIM_HYP ? 1u : 0u;
+              lput(gs.hyp, gid, hyp0);
               lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
               lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
             }
@@ -761,11 +771,20 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
       }
     }
   }
+  // RRT_CLAIM_HYP 2: a listed pixel's hint bit (31) = its central camera ray is no proven miss
+  // (the batch kernel's first hypothesis for the pixel)
+  uint32_t hint = 0u;
+  if (RRT_CLAIM_HYP == 2 && listed) {
+    const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+    const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
+    Counters cn = {};
+    hint = camera_miss_proof<false>(kp, ld3(kp.cam.pos), pixel_ray_dir(kp, x + 0.5, y + 0.5), cn) ? 0u : 1u;
+  }
   const uint64_t b = __ballot(listed);
   uint32_t base = 0;
   if (lane == 0 && b) base = atomicAdd(kp.claim_count, (uint32_t)__popcll(b));
   base = __shfl(base, 0);
-  if (listed) kp.claim_list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = ix;
+  if (listed) kp.claim_list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = ix | (hint << 31);
 }
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream) {
   hipLaunchKernelGGL(rrt_pixel_proof_kernel, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_kp);
