@@ -320,10 +320,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
 template <int LEAN>
 struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
+#ifndef RRT_STRIPE
 #define RRT_STRIPE 16  // striped claim queues: runs of consecutive claims (neighbouring pixels)
+#endif
 #ifndef RRT_CLAIM_HYP
-#define RRT_CLAIM_HYP 1  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
-                         // proof pass's hint (A/B: cfg3 23.9 / 22.7 ms for 0 / 1)
+#define RRT_CLAIM_HYP 2  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
+                         // proof pass's hint (A/B: cfg3 23.9 / 22.6 / 20.5 ms, cfg4 - / 19.8 / 20.1)
 #endif
 #ifndef RRT_TAIL_PRIO
 #define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
