@@ -321,7 +321,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 template <int LEAN>
 struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
 #ifndef RRT_STRIPE
-#define RRT_STRIPE 16  // striped claim queues: runs of consecutive claims (neighbouring pixels)
+#define RRT_STRIPE 32  // striped claim queues: runs of consecutive claims (neighbouring pixels; A/B
+                       // cfg3 20.1 ms at 32, 20.6 at 16, 20.7 at 8)
 #endif
 #ifndef RRT_CLAIM_HYP
 #define RRT_CLAIM_HYP 2  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
