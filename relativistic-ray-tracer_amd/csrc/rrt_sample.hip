@@ -855,6 +855,7 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
     switch (waves) {
       case 2: RRT_LAUNCH_B(1, 2); break;
       case 3: RRT_LAUNCH_B(1, 3); break;
+      case 4: RRT_LAUNCH_B(1, 4); break;
       case 5: RRT_LAUNCH_B(1, 5); break;
       case 6: RRT_LAUNCH_B(1, 6); break;
       default: RRT_LAUNCH_B(1, 5); break;
