@@ -320,9 +320,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
 template <int LEAN>
 struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128u; };
+// striped claim queues: runs of RRT_STRIPE_OF(V) consecutive claims (neighbouring pixels).
+// Interleaved A/B (ms/frame): cfg3 (build 1) 20.2 at 32, 20.7 at 16, 20.7 at 8; cfg4 (build 2)
+// 20.6 at 32, 20.0 at 16.
 #ifndef RRT_STRIPE
-#define RRT_STRIPE 32  // striped claim queues: runs of consecutive claims (neighbouring pixels; A/B
-                       // cfg3 20.1 ms at 32, 20.6 at 16, 20.7 at 8)
+#define RRT_STRIPE_OF(V) ((V) == 2 ? 16u : 32u)
+#else
+#define RRT_STRIPE_OF(V) ((uint32_t)RRT_STRIPE)
 #endif
 #ifndef RRT_CLAIM_HYP
 #define RRT_CLAIM_HYP 2  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
@@ -355,6 +359,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   using namespace rrt;
   __shared__ ShadeLds cl;
   constexpr uint32_t RRT_SLOTS = SlotWindow<LEAN>::n;
+  constexpr uint32_t STRIPE = RRT_STRIPE_OF(LEAN);
   __shared__ GroupLds<RRT_SLOTS> gs;
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
   float* const fg = cl.cg;
@@ -390,7 +395,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       // claim space: every pixel slot, or the pixel proof's list padded to whole stripes (the
       // padding claims no pixel); read here, not held through the kernel
       const uint32_t n_list = kp.claim_list ? *kp.claim_count : 0u;
-      const uint32_t npx = kp.claim_list ? (n_list + RRT_STRIPE - 1) / RRT_STRIPE * RRT_STRIPE : kp.n_pixels;
+      const uint32_t npx = kp.claim_list ? (n_list + STRIPE - 1) / STRIPE * STRIPE : kp.n_pixels;
       uint64_t pending = needers;
       uint32_t p = npx + 1;  // npx + 1: this group did not claim
       while (pending) {
@@ -400,11 +405,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
           if (q_left == 0) {  // every queue found empty before
             out = 1;
           } else {
-            // striped queues: queue q holds the runs q, q + nq, q + 2 nq, ... of RRT_STRIPE
+            // striped queues: queue q holds the runs q, q + nq, q + 2 nq, ... of STRIPE
             // consecutive claims (n_pixels is a multiple of 64: tiles of 8k x 8k pixels)
             const uint32_t nq = kp.n_queues;
             const uint32_t qb = kp.q_stripe ? 0u : (q ? kp.q_end[q - 1] : 0u);
-            const uint32_t qn = kp.q_stripe ? (npx / RRT_STRIPE - q + nq - 1) / nq * RRT_STRIPE
+            const uint32_t qn = kp.q_stripe ? (npx / STRIPE - q + nq - 1) / nq * STRIPE
                                             : (kp.claim_list ? npx : kp.q_end[q] - qb);
             const uint32_t k = atomicAdd(kp.block_counter + RRT_QUEUE_STRIDE * q, want);
             if (k < qn) {
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         const bool mine = (pending >> gbase) & 1ull;
         if (mine && rank < got) {
           const uint32_t ix = base + rank;
-          p = kp.q_stripe ? ((ix / RRT_STRIPE) * kp.n_queues + qc) * RRT_STRIPE + ix % RRT_STRIPE : ix;
+          p = kp.q_stripe ? ((ix / STRIPE) * kp.n_queues + qc) * STRIPE + ix % STRIPE : ix;
         }
         if (mine && out) p = npx;
         pending = out ? 0ull : (got >= want ? 0ull : pending & ~__ballot(gl == 0 && mine && rank < got));
