@@ -19,9 +19,6 @@
 #include "../../include/rrt.h"
 #include "../../include/rrt_scene_format.h"
 #include "rrt_internal.h"
-#ifndef RRT_CLAIM_HINT_ALL
-#define RRT_CLAIM_HINT_ALL 0  // 1: the first-hypothesis hint for the point-light build too (A/B)
-#endif
 #include "rrt_scene_file.h"
 
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
@@ -1185,7 +1182,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
     kp.tile_order = c->d_order;
     kp.first = nullptr;
-    kp.claim_list = nullptr; kp.claim_count = nullptr; kp.claim_hint = 0u;
+    kp.claim_list = nullptr; kp.claim_count = nullptr;
     // sample-0 pre-pass: off by default (with the slot speculation a wrong first hypothesis
     // costs one round, less than the extra pass; tools/ab_kernels.py cfg3 46.4 vs 47.8 ms)
     if ((p->flags & RRT_RENDER_PREPASS) && !(p->flags & RRT_RENDER_NO_FIRST)) {
@@ -1207,9 +1204,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         c->list_cap = kp.n_pixels;
       }
       kp.claim_list = c->d_list;
-      // the hint pays on the area-light build (cfg3 22.6 -> 20.5 ms); on the point-light build
-      // the extra proof in the pass cost more than it saved (cfg4 19.8 vs 20.1 ms): "hit" there
-      kp.claim_hint = (lean == 1 || RRT_CLAIM_HINT_ALL) ? 1u : 0u;
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
     }
   }

@@ -188,7 +188,6 @@ struct KParams {
   uint32_t draws_miss;   // RNG draws of a camera sample whose query misses (jitter: 2)
   uint32_t draws_hit;    // ... and of one that hits (jitter + the direct-lighting sampler draws)
   uint32_t clip_x0, clip_y0, clip_x1, clip_y1;  // region actually requested (exclusive end)
-  uint32_t claim_hint;  // 1: the pixel proof pass writes the first-hypothesis hint (bit 31)
   // outputs, packed per tile: pixel (i, j) of tile t at t*tile_size^2 + j*tile_size + i
   float* rgb;
   int32_t* count;

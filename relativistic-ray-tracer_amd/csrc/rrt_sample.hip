@@ -468,12 +468,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
               lput(gs.O, gid, 0u); lput(gs.i, gid, 0u);
               // The first step's hypothesis: "miss" without the pixel proof's list; for a listed
               // pixel (one whose camera rays are not all proven misses) RRT_CLAIM_HYP 1 takes
-              // "hit", 2 the list entry's hint (its central ray is no proven miss) where the pass
-              // wrote one (KParams::claim_hint), else "hit"
-              const uint32_t hyp0 = !kp.claim_list           ? 0u
-                                    : RRT_CLAIM_HYP == 2 && kp.claim_hint ? (ent >> 31)
-                                    : RRT_CLAIM_HYP                  ? 1u
-                                                                     : 0u;
+              // "hit", 2 the list entry's hint (its central ray is no proven miss)
+              const uint32_t hyp0 = !kp.claim_list ? 0u : RRT_CLAIM_HYP == 2 ? (ent >> 31) : RRT_CLAIM_HYP ? 1u : 0u;
               lput(gs.hyp, gid, hyp0);
               lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
               lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
@@ -786,7 +782,7 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
   // RRT_CLAIM_HYP 2: a listed pixel's hint bit (31) = its central camera ray is no proven miss
   // (the batch kernel's first hypothesis for the pixel)
   uint32_t hint = 0u;
-  if (RRT_CLAIM_HYP == 2 && listed && kp.claim_hint) {
+  if (RRT_CLAIM_HYP == 2 && listed) {
     const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
     const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
     Counters cn = {};
