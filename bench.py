@@ -24,6 +24,8 @@ Prints ONE JSON line (rank 0).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,9 +33,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
-
-import rrt  # noqa: E402
-import rrt_frame  # noqa: E402
+# rrt / rrt_frame (librrt.so) are imported in main(), after the rank launcher: the parent of a
+# multi-rank run must not load the HIP library or touch the GPU before its ranks start
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
@@ -84,6 +85,91 @@ BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic byte
 BYTES_PLANE = 32  # plane-cull record (DPlane) read per plane test
 
 
+# MI355X FP64 vector peak (spec, AMD MI355X datasheet: 78.6 TFLOP/s FP64 vector = 256 CUs x
+# 128 flop/clk x 2.4 GHz, i.e. a wave64 FP64 FMA every 4 cycles per SIMD; tools/ubench_f64.hip
+# measures that issue rate on the box, profiles/r03_ubench_f64.log)
+FP64_PEAK_TFLOPS = 78.6
+FP64_CYCLES_PER_WAVE_INST = 4.0
+N_SIMD = 1024
+
+
+def find_profile(explicit, names, workload, kernel):
+    """The first profiles/ JSON (or the explicit path) recorded for this workload and kernel --
+    numbers from another kernel build are never attached to this run's line."""
+    paths = [explicit] if explicit else [os.path.join(ROOT, "profiles", n) for n in names]
+    for path in paths:
+        if path and os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("workload") == workload and kernel in (d.get("kernel"), d.get("main_kernel")):
+                d["_path"] = os.path.relpath(path, ROOT)
+                return d
+    return None
+
+
+def rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc):
+    """The dominant kernel against its real bound, FP64 VALU issue (PMC, profiles/r03_*_pmc.json),
+    and against HBM on the survey's algorithmic bytes, both per launch of that
+    kernel over its HIP-event time in this run.  The algorithmic bytes are reads of a scene that
+    stays L2/MALL-resident, so the HBM line's `traffic` (PMC FETCH/WRITE of the same kernel,
+    split into register-spill scratch and the rest) is what HBM actually moved."""
+    t = main_ms * 1e-3
+    hbm_ach = loc_bytes / t / 1e9
+    src = pmc if (pmc and pmc.get("hbm_bytes") is not None) else traffic
+    hbm = {"bound": "hbm", "achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
+           "traffic": src.get("hbm_bytes", src.get("hbm_bytes_per_launch")) if src else None,
+           "traffic_scratch": src.get("scratch_bytes") if src else None,
+           "traffic_other": src.get("other_bytes") if src else None,
+           "traffic_source": src["_path"] if src else None,
+           "kernel": main_kernel, "kernel_ms": main_ms, "launch": kernel_name,
+           "algorithmic_bytes_per_launch": float(loc_bytes),
+           "reference_algorithm_bytes_per_launch": float(ref_bytes),
+           "reference_equivalent_GBps": ref_bytes / t / 1e9}
+    out = {"roofline_hbm": hbm}
+    if pmc:
+        flops = pmc["fp64_flops_per_launch"]
+        ach = flops / t / 1e12
+        insts = pmc["fp64_wave_insts_per_launch"]
+        clk = pmc.get("clock_hz") or 2.4e9
+        out["roofline"] = {
+            "bound": "fp64_valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / FP64_PEAK_TFLOPS, "traffic": hbm["traffic"], "kernel": main_kernel, "kernel_ms": main_ms,
+            "fp64_flops_per_launch": flops, "fp64_wave_insts_per_launch": insts,
+            "valu_lane_util": pmc["valu_lane_util"],
+            # share of the chip's FP64 issue slots (a wave64 FP64 op per 4 cycles per SIMD) used
+            "fp64_issue_frac": insts * FP64_CYCLES_PER_WAVE_INST / (N_SIMD * clk * t),
+            "valu_busy_frac": pmc.get("valu_busy_frac"),
+            "source": pmc["_path"]}
+    else:
+        out["roofline"] = dict(hbm, note="no PMC profile of this kernel build: HBM line only")
+    return out
+
+
+def host_cores():
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota (the GPU
+    box's share of its host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(wl, threads, row_stride, scene_path, camera_path, env=None):
     """The oracle restatement (oracle/restate, bit-exact with the reference) on the host cores,
     over every `row_stride`-th row of the same frame (a representative bounded sample)."""
@@ -102,10 +188,67 @@ def cpu_baseline(wl, threads, row_stride, scene_path, camera_path, env=None):
         _, cnt, _, _ = O.render(s, cam, p, 0, y, wl["w"], 1, threads=threads)
         samples += int(cnt.sum())
     dt_s = time.perf_counter() - t0
-    return {"value": samples / dt_s / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"rows {rows[0]}::{row_stride} of the {wl['w']}x{wl['h']} frame ({len(rows)} rows, "
-                      f"{samples} samples, {dt_s:.1f} s); oracle/restate (C, bit-exact with the reference "
-                      f"under the keyed RNG), pthreads over 32-px tiles"}
+    out = {"value": samples / dt_s / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "host_cores_visible": os.cpu_count(),
+           "sample": f"rows {rows[0]}::{row_stride} of the {wl['w']}x{wl['h']} frame ({len(rows)} rows, "
+                     f"{samples} samples, {dt_s:.1f} s); oracle/restate (C, bit-exact with the reference "
+                     f"under the keyed RNG), pthreads over 32-px tiles"}
+    # the restatement's speed relative to the compiled reference on the same cores and sample,
+    # measured in the build container (tools/cpu_ratio.py; the reference does not travel here)
+    ratio_path = os.path.join(ROOT, "profiles", "r03_cpu_ratio.json")
+    if os.path.exists(ratio_path):
+        with open(ratio_path) as f:
+            rr = json.load(f).get(wl_name(wl))
+        if rr:
+            out["restatement_over_reference_speed"] = rr["speed_ratio"]
+            out["reference_equivalent_value"] = out["value"] / rr["speed_ratio"]
+            out["ratio_measured"] = rr["where"]
+    return out
+
+
+def wl_name(wl):
+    return next(k for k, v in WORKLOADS.items() if v is wl)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_cmd(argv, n, port):
+    """The torchrun command that runs this script as n ranks on one node (the driver's own form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env=None):
+    """How this process takes part in a --gpus N run: "launch" (no WORLD_SIZE and N > 1: start the
+    N ranks), "rank" (one of WORLD_SIZE == N ranks) or "single".  A WORLD_SIZE that disagrees
+    with --gpus is an error, never a relabelled run."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} < 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "single"
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}")
+    return "rank" if gpus > 1 else "single"
+
+
+def launch_ranks(gpus, argv):
+    """Parent of a multi-GPU run (pathtracer.cpp:279-281 starts one worker per thread; here one
+    process per GPU): checks the GPU count WITHOUT initialising HIP (torch.cuda.device_count()
+    does not, on this image), starts the ranks with torchrun and returns its exit code.  Rank 0
+    prints the JSON line straight to this process's stdout."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < gpus:
+        raise SystemExit(f"bench.py --gpus {gpus}: only {n} GPU(s) visible")
+    return subprocess.run(rank_launch_cmd(argv, gpus, _free_port())).returncode
 
 
 def main():
@@ -120,9 +263,19 @@ def main():
     ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--traffic", default=None,
                     help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic; "
-                         "default profiles/r02_traffic.json (cfg3) or profiles/r02_traffic_<workload>.json")
+                         "default profiles/r03_traffic_<workload>.json")
+    ap.add_argument("--pmc", default=None,
+                    help="PMC FP64 VALU counters per launch (tools/pmc_valu.py) for the fp64_valu roofline; "
+                         "default profiles/r03_<workload>_pmc.json")
     a = ap.parse_args()
 
+    mode = check_world(a.gpus)
+    if mode == "launch":
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+
+    global rrt, rrt_frame
+    import rrt
+    import rrt_frame
     import torch
     import torch.distributed as dist
 
@@ -130,8 +283,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        if torch.cuda.device_count() <= local:
+            raise SystemExit(f"bench.py rank {rank}: no GPU for local rank {local}")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -198,6 +354,10 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     k_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kern_ms]))
+    # the timed launches' own HIP events (recorded by librrt on this stream around each launch and
+    # before its main kernel): the dominant kernel's average duration, for the roofline
+    tot_ms, main_ms = r.launch_times(min(a.steps, 32))
+    main_ms = float(np.mean(main_ms))
 
     kernel_name = r.stats().kernel.decode()
 
@@ -224,22 +384,15 @@ def main():
     (_, x_bbox, x_micro, x_prim, x_plane, _), xc4 = count_pass(rrt.RRT_RENDER_COUNT_EXECUTED)
     loc_bytes = BYTES_AABB * xc4[0] + BYTES_PRIM * xc4[2] + BYTES_PLANE * xc4[3] + BYTES_PIXEL * pix_local
     ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
-    traffic = None
-    if a.traffic is None:
-        a.traffic = os.path.join(ROOT, "profiles", "r02_traffic.json" if a.workload == "cfg3"
-                                 else f"r02_traffic_{a.workload}.json")
-    if os.path.exists(a.traffic):
-        with open(a.traffic) as f:
-            tr = json.load(f)
-        if tr.get("workload") == a.workload and tr.get("kernel") == kernel_name:
-            traffic = tr["hbm_bytes_per_launch"]
+    main_kernel = kernel_name.split(" + ")[-1]
+    traffic = find_profile(a.traffic, [f"r03_traffic_{a.workload}.json"], a.workload, kernel_name)
+    pmc = find_profile(a.pmc, [f"r03_{a.workload}_pmc.json"], a.workload, main_kernel)
 
     if rank == 0:
         # sanity: the gathered frame holds every pixel's sample count
         frame_samples = int(frame_cnt.to(torch.int64).sum().item())
         assert frame_samples == int(samples), (frame_samples, samples)
         value = samples * a.steps / elapsed / 1e6
-        achieved = loc_bytes / (k_ms * 1e-3) / 1e9
         work = {"aabb_tests": bbox / samples, "micro_steps": micro / samples, "prim_tests": prim / samples,
                 "queries": queries / samples}
         xwork = {"aabb_tests": x_bbox / samples, "micro_steps": x_micro / samples, "prim_tests": x_prim / samples,
@@ -265,17 +418,13 @@ def main():
             "samples_per_frame": int(samples),
             "nominal_msamples_per_s": W * H * wl["spp"] * a.steps / elapsed / 1e6,
             "kernel_ms_rank0": k_ms,
+            "main_kernel_ms_rank0": main_ms,
             "work_per_sample_reference": work,
             "work_per_sample_executed": xwork,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel_name,
-                         "algorithmic_bytes_per_launch": float(loc_bytes),
-                         "reference_algorithm_bytes_per_launch": float(ref_bytes),
-                         "reference_equivalent_GBps": ref_bytes / (k_ms * 1e-3) / 1e9},
         }
+        out.update(rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc))
         if world == 1 and not a.no_cpu_baseline:
-            threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+            threads = a.cpu_threads or host_cores()
             out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride or wl["row_stride"], scene_path,
                                                camera_path, env)
         print(json.dumps(out), flush=True)

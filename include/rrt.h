@@ -249,8 +249,13 @@ typedef struct {
   float last_kernel_ms;       /* HIP-event time of the last render launch */
   uint32_t grid_blocks, block_threads;
   char kernel[64];            /* name of the last render kernel(s) launched */
+  float last_main_kernel_ms;  /* HIP-event time of the last launch's main kernel alone (after
+                                 any pre-pass such as rrt_pixel_proof_kernel) */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
+/* HIP-event times of the last n (<= 32) render launches, oldest first: the whole launch and its
+ * main kernel alone (bench.py's roofline divides by the latter).  Returns the count filled. */
+int rrt_get_launch_times(const rrt_ctx* ctx, uint32_t n, float* total_ms, float* main_ms);
 /* Host copy of the flattened BVH: boxes [n][6] (min, max), nodes [n][4] (first, count, left,
  * right; count 0 = inner node), prims [n_leaf_refs] (build-order primitive ids) -- the layout
  * of the oracle's reference-BVH dump.  Any pointer may be NULL to query sizes via stats. */

@@ -14,6 +14,7 @@
 //   sampler  UniformGrid / CosineWeighted / UniformHemisphere / UniformSphere  sampler.cpp:7-56
 //   bsdf     Diffuse / Mirror / Glass / Microfacet sample_f    part1_code.cpp:167-173, bsdf.cpp:33-140
 //   area     AreaLight::sample_L                               light.cpp:80-92
+//   light    Point / Directional / InfiniteHemisphere sample_L  light.cpp:17-23, 34-42, 49-57
 //   camray   Camera::generate_ray                              part1_code.cpp:182-187
 #include <cmath>
 #include <cstring>
@@ -298,6 +299,44 @@ int main(int argc, char** argv) {
              cam.c2w[0].x, cam.c2w[0].y, cam.c2w[0].z, cam.c2w[1].x, cam.c2w[1].y, cam.c2w[1].z,
              cam.c2w[2].x, cam.c2w[2].y, cam.c2w[2].z, cam.nClip, cam.fClip, x, y,
              r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.min_t, r.max_t});
+    }
+    t.save();
+  }
+
+  // ---- light: the other lights' sample_L (light.cpp:17-23 directional, :34-42 infinite
+  // hemisphere, :49-57 point), scripted draws.  row: kind (1 point, 2 directional, 3 hemisphere),
+  // rad3, ctor argument3 (point position / directional lightDir; unused for the hemisphere),
+  // the light's own vector (PointLight::position / DirectionalLight::dirToLight), p3,
+  // rand ints(2) -> L3 wi3 dist pdf draws
+  {
+    Table t{"light", 1 + 3 + 3 + 3 + 3 + 2 + 3 + 3 + 3};
+    for (int k = 0; k < 768; ++k) {
+      const int kind = 1 + k % 3;
+      Spectrum rad((float)urange(0, 5), (float)urange(0, 5), (float)urange(0, 5));
+      Vector3D arg = uvec(-2, 2), p = uvec(-1, 1);
+      if (k % 24 == 2) arg = Vector3D(0, -1, 0);  // straight down, as the scenes' sun
+      std::vector<int> s = {rint31(), rint31()};
+      if (k % 48 == 5) s = {0, 0};
+      if (k % 48 == 8) s = {2147483647, 2147483647};
+      script(s);
+      Vector3D wi, own;
+      float dist = -1, pdf = -1;
+      Spectrum L;
+      if (kind == 1) {
+        StaticScene::PointLight l(rad, arg);
+        own = l.position;
+        L = l.sample_L(p, &wi, &dist, &pdf);
+      } else if (kind == 2) {
+        StaticScene::DirectionalLight l(rad, arg);
+        own = l.dirToLight;
+        L = l.sample_L(p, &wi, &dist, &pdf);
+      } else {
+        StaticScene::InfiniteHemisphereLight l(rad);
+        L = l.sample_L(p, &wi, &dist, &pdf);
+      }
+      t.row({(double)kind, rad.r, rad.g, rad.b, arg.x, arg.y, arg.z, own.x, own.y, own.z, p.x, p.y, p.z,
+             (double)s[0], (double)s[1], L.r, L.g, L.b, wi.x, wi.y, wi.z, (double)dist, (double)pdf,
+             (double)g_rng.ctr});
     }
     t.save();
   }

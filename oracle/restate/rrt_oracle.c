@@ -1180,6 +1180,18 @@ void ro_area_sample(const float* rad, const double* v, const double* p, const in
   spec s = light_sample_L(NULL, &l, &g, V(p[0], p[1], p[2]), &w, dist, pdf);
   L[0] = s.r; L[1] = s.g; L[2] = s.b; wi[0] = w.x; wi[1] = w.y; wi[2] = w.z;
 }
+/* point (1) / directional (2) / infinite hemisphere (3) lights' sample_L (light.cpp:17-57) */
+void ro_light_sample(int type, const float* rad, const double* v, const double* p, const int* rands, float* L,
+                     double* wi, float* dist, float* pdf, int* used) {
+  light_t l; memset(&l, 0, sizeof(l));
+  l.type = (uint32_t)type; l.rad[0] = rad[0]; l.rad[1] = rad[1]; l.rad[2] = rad[2];
+  for (int k = 0; k < 4; ++k) l.v[k] = V(v[3 * k], v[3 * k + 1], v[3 * k + 2]);
+  rng_t g; memset(&g, 0, sizeof(g)); g.script = rands; g.script_len = 2;
+  v3 w;
+  spec s = light_sample_L(NULL, &l, &g, V(p[0], p[1], p[2]), &w, dist, pdf);
+  L[0] = s.r; L[1] = s.g; L[2] = s.b; wi[0] = w.x; wi[1] = w.y; wi[2] = w.z;
+  *used = (int)g.ctr;
+}
 void ro_camera_ray(double hFov, double vFov, const double* pos, const double* c2w, double nClip, double fClip,
                    double x, double y, double* o, double* d, double* min_t, double* max_t) {
   pctx c; memset(&c, 0, sizeof(c));

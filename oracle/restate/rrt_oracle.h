@@ -89,6 +89,9 @@ void ro_bsdf_sample(int kind, const double* prm /*8*/, const double* wo, const i
                     double* wi, float* pdf, int* used, float* feval3);
 void ro_area_sample(const float* rad, const double* v /*12*/, const double* p, const int* rands, float* L,
                     double* wi, float* dist, float* pdf);
+/* light types 1 point, 2 directional, 3 infinite hemisphere (v: the light's 4 vectors) */
+void ro_light_sample(int type, const float* rad, const double* v /*12*/, const double* p, const int* rands, float* L,
+                     double* wi, float* dist, float* pdf, int* used);
 void ro_camera_ray(double hFov, double vFov, const double* pos, const double* c2w_cols /*9*/, double nClip,
                    double fClip, double x, double y, double* o, double* d, double* min_t, double* max_t);
 

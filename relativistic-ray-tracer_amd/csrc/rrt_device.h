@@ -1141,19 +1141,19 @@ __device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px,
     const double m0 = mp.eta * (fmax(rp, r) + mp.scale);
     const double m = m0 + fmax(dpa, dpb);
     // Distance from the hole: a ray's segment depends only on its (v_prev, v) -- turning the
-    // plane about x keeps it -- and the pixel's pairs lie in [v_prev +- dvp] x [v +- dv]; the
-    // camera proof's scalar test must hold at the four corners of that box.  D is convex there
-    // (its maximum, the nearest line, at a corner) and |v|, |v_prev| are largest at corners.
+    // plane about x keeps it -- and the pixel's pairs lie in [v_prev +- dvp] x [v +- dv], a box
+    // on which neither coordinate changes sign (checked above, and for v_prev one step earlier).
+    // A segment is never nearer the hole than its line, at distance^2 sin^2 dt / D, and D is a
+    // positive definite quadratic form on that box (convex: its maximum, the nearest line, at a
+    // corner), so the line test at the four corners covers every ray of the pixel, whichever
+    // side of its segment the foot of the perpendicular falls on.
     const double rb = mp.r_ball + m0;
     bool far = true;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const double w = v[1] + ((k & 1) ? dv : -dv), wp = vp[1] + ((k & 2) ? dvp : -dvp);
-      const double aw = fabs(w), awp = fabs(wp);
-      const double D = w * w + wp * wp - 2.0 * mp.co1 * awp * w;
-      const bool inside = w * (mp.co1 * awp - w) < 0.0 && awp * (awp - mp.co1 * w) > 0.0;
-      far = far && (inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(w * w, wp * wp));
-      (void)aw;
+      const double D = w * w + wp * wp - 2.0 * mp.co1 * fabs(wp) * w;
+      far = far && si2 > rb * rb * D;
     }
     if (!far) {
       const double ia = mp.rho / vp[1], ib = mp.rho / v[1];

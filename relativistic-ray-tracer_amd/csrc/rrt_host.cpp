@@ -84,7 +84,11 @@ struct rrt_ctx {
   int device = -1;
   std::string err;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // per-launch timing ring: ev0 before the launch, ev_main before its main kernel (after any
+  // pre-pass), ev1 after it; slot = launch number % kRing
+  static constexpr uint32_t kRing = 32;
+  hipEvent_t ev0[kRing] = {}, ev_main[kRing] = {}, ev1[kRing] = {};
+  uint64_t n_launch = 0;
   // scratch fence: every launch and unpack rewrites the per-context workspace below (KParams,
   // claim counters, tile list/order, sample-0 slots) with async copies on the caller's stream;
   // a use on a different stream than the previous one first waits for this event
@@ -151,7 +155,7 @@ struct rrt_ctx {
   size_t first_cap = 0;
   float* d_rgb = nullptr; int32_t* d_cnt = nullptr; uint32_t* d_draws = nullptr; uint32_t* d_ctr = nullptr;
   size_t px_cap = 0;
-  float last_ms = 0.f;
+  float last_ms = 0.f, last_main_ms = 0.f;
   bool timed = false;
   uint32_t last_grid = 0;
   std::string last_kernel;
@@ -184,6 +188,15 @@ static void free_scene_dev(rrt_ctx* c) {
   c->device_bytes = 0;
 }
 
+
+static bool create_ring(rrt_ctx* c) {
+  for (uint32_t i = 0; i < rrt_ctx::kRing; ++i)
+    if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev_main[i]) != hipSuccess ||
+        hipEventCreate(&c->ev1[i]) != hipSuccess)
+      return false;
+  return true;
+}
+
 extern "C" {
 
 int rrt_abi_version(void) { return RRT_ABI_VERSION; }
@@ -203,7 +216,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        !create_ring(c.get()) ||
         hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counter, kCounterBytes) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
@@ -223,8 +236,11 @@ void rrt_destroy(rrt_ctx* c) {
     free_env_dev(c);
     hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_list); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
+    for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
+      if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
+      if (c->ev_main[i]) hipEventDestroy(c->ev_main[i]);
+      if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
+    }
     if (c->ev_fence) hipEventDestroy(c->ev_fence);
     if (c->stream) hipStreamDestroy(c->stream);
   }
@@ -976,6 +992,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (n_tiles == 0) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = scratch_acquire(c, stream)) return rc;
+  // whatever path leaves this function, the work already enqueued on `stream` fences the
+  // workspace for the next user on another stream
+  struct FenceGuard {
+    rrt_ctx* c; hipStream_t s;
+    ~FenceGuard() { scratch_release(c, s); }
+  } fence_guard{c, stream};
   if (c->tiles_cap < n_tiles) {
     // hipFree waits for the device, so no launch still reads the old list
     hipFree(c->d_tiles); c->d_tiles = nullptr;
@@ -1019,6 +1041,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     kp.hole.r_esc2 = e2 > f2 ? e2 : f2;
     kp.hole.kerr_max_steps = 4 * kp.hole.steps;
   }
+  bool proofs_valid = false;
   {  // camera-ray miss proof constants (rrt_device.h camera_miss_proof)
     const DHole& h = kp.hole;
     DMissProof& mp = kp.miss;
@@ -1045,10 +1068,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     mp.r_ball = std::sqrt(rb2) * (1.0 + 1e-9);
     bool fin = std::isfinite(mp.scale) && std::isfinite(h.r) && h.r >= 0.0;
     for (int k = 0; k < 3; ++k) fin = fin && std::isfinite(h.c[k]);
-    // the recurrence needs a proper turn per step (0 < dt < pi, sin dt > 0)
-    mp.on = (h.kind == RRT_METRIC_SCHWARZSCHILD && fin && h.dt > 0.0 && h.dt < 3.0 && h.sin_dt > 0.0 &&
-             h.steps >= 1 && !(p->flags & RRT_RENDER_NO_MISS_PROOF))
-                ? 1u : 0u;
+    // the recurrence needs a proper turn per step (0 < dt < pi, sin dt > 0); the three proofs
+    // share these constants, and each has its own switch below
+    proofs_valid = h.kind == RRT_METRIC_SCHWARZSCHILD && fin && h.dt > 0.0 && h.dt < 3.0 && h.sin_dt > 0.0 &&
+                   h.steps >= 1;
+    mp.on = (proofs_valid && !(p->flags & RRT_RENDER_NO_MISS_PROOF)) ? 1u : 0u;
   }
   {  // shadow-ray occlusion proof: the same recurrence, against the root box's face triangles
     kp.occ = c->occ;
@@ -1064,7 +1088,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
     // the point-light scenes' builds carry no proof (rrt_sample.hip RRT_OCC_TAG); off for them in
     // every kernel, so the counting passes count what their batch kernel executes
-    kp.occ.on = (kp.miss.on && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
+    kp.occ.on = (proofs_valid && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
   }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;
@@ -1196,7 +1220,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // pixel miss proof pass (rrt_pixel_proof_kernel): the area/point-light builds, whose misses
     // are black, with a claim order it can compact (striped or one queue); list entries keep bit
     // 31 for the first-hypothesis hint
-    if ((lean == 1 || lean == 2) && kp.miss.on && !c->env_w && !kp.first && (striped || nq == 1) &&
+    // The pass writes a proven pixel's result as the first adaptive check's stop on all-zero
+    // samples, which holds only when 1.96 * 0 <= max_tolerance * 0 (a finite tolerance; with an
+    // infinite or NaN one the reference runs all ns_aa samples, part1_code.cpp:147-158)
+    const bool zero_stops = 0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2;
+    if ((lean == 1 || lean == 2) && proofs_valid && zero_stops && !c->env_w && !kp.first && (striped || nq == 1) &&
         kp.n_pixels < 0x80000000u && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
       if (c->list_cap < kp.n_pixels) {
         hipFree(c->d_list); c->d_list = nullptr;
@@ -1212,7 +1240,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (grid == 0) grid = 1;
   c->last_grid = grid;
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
-  HIPCHK(c, hipEventRecord(c->ev0, stream));
+  const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
+  HIPCHK(c, hipEventRecord(c->ev0[ring], stream));
   const char* tf[2] = {"false", "true"};
   char name[96];
   if (batch) {
@@ -1231,21 +1260,26 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, fw, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
     if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
   } else if (mega) {
     std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
+    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %d, ...>", tf[deep], tf[count], lean == 2 ? 0 : lean);
+    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {
     std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %d, ...>", tf[count], lean);
+    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }
   c->last_kernel = name;
-  HIPCHK(c, hipEventRecord(c->ev1, stream));
+  HIPCHK(c, hipEventRecord(c->ev1[ring], stream));
   c->timed = true;
-  return scratch_release(c, stream);
+  ++c->n_launch;
+  return RRT_OK;
 }
 
 extern "C" int rrt_render_tiles_device(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
@@ -1264,6 +1298,10 @@ extern "C" int rrt_unpack_tiles_device(rrt_ctx* c, const uint32_t* tiles, uint32
   hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)0;
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = scratch_acquire(c, s)) return rc;
+  struct FenceGuard {
+    rrt_ctx* c; hipStream_t s;
+    ~FenceGuard() { scratch_release(c, s); }
+  } fence_guard{c, s};
   if (c->tiles_cap < n_tiles) {
     hipFree(c->d_tiles); c->d_tiles = nullptr;
     HIPCHK(c, hipMalloc(&c->d_tiles, sizeof(uint32_t) * 2 * n_tiles));
@@ -1271,7 +1309,7 @@ extern "C" int rrt_unpack_tiles_device(rrt_ctx* c, const uint32_t* tiles, uint32
   }
   HIPCHK(c, hipMemcpyAsync(c->d_tiles, tiles, sizeof(uint32_t) * 2 * n_tiles, hipMemcpyHostToDevice, s));
   HIPCHK(c, rrt_launch_unpack(c->d_tiles, n_tiles, ts, fw, fh, rgb_p, cnt_p, rgb, cnt, s));
-  return scratch_release(c, s);
+  return RRT_OK;
 }
 
 extern "C" int rrt_tonemap_device(rrt_ctx* c, uint32_t n, const float* rgb, uint32_t* rgba, void* stream) {
@@ -1361,13 +1399,34 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
   out->block_threads = 256;
   if (c->device >= 0 && c->timed) {
     hipSetDevice(c->device);
-    if (hipEventSynchronize(c->ev1) == hipSuccess) {
+    const uint32_t last = (uint32_t)((c->n_launch + rrt_ctx::kRing - 1) % rrt_ctx::kRing);
+    if (hipEventSynchronize(c->ev1[last]) == hipSuccess) {
       float ms = 0;
-      if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_ms = ms;
+      if (hipEventElapsedTime(&ms, c->ev0[last], c->ev1[last]) == hipSuccess) c->last_ms = ms;
+      if (hipEventElapsedTime(&ms, c->ev_main[last], c->ev1[last]) == hipSuccess) c->last_main_ms = ms;
     }
   }
   out->last_kernel_ms = c->last_ms;
+  out->last_main_kernel_ms = c->last_main_ms;
   return RRT_OK;
+}
+
+// Per-launch HIP-event times of the context's last n launches (n <= 32), oldest first: the whole
+// launch and its main kernel alone.  Synchronises on the last of them.  Returns the count filled.
+extern "C" int rrt_get_launch_times(const rrt_ctx* cc, uint32_t n, float* total_ms, float* main_ms) {
+  rrt_ctx* c = const_cast<rrt_ctx*>(cc);
+  if (!c || (n && (!total_ms || !main_ms))) return RRT_E_INVALID;
+  if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "no device");
+  const uint64_t have = std::min<uint64_t>(c->n_launch, rrt_ctx::kRing);
+  const uint32_t k = (uint32_t)std::min<uint64_t>(n, have);
+  HIPCHK(c, hipSetDevice(c->device));
+  for (uint32_t i = 0; i < k; ++i) {
+    const uint32_t slot = (uint32_t)((c->n_launch - k + i) % rrt_ctx::kRing);
+    HIPCHK(c, hipEventSynchronize(c->ev1[slot]));
+    HIPCHK(c, hipEventElapsedTime(&total_ms[i], c->ev0[slot], c->ev1[slot]));
+    HIPCHK(c, hipEventElapsedTime(&main_ms[i], c->ev_main[slot], c->ev1[slot]));
+  }
+  return (int)k;
 }
 
 extern "C" int rrt_get_free_grid(const rrt_ctx* c, uint8_t* k, double* geom, int32_t* n) {

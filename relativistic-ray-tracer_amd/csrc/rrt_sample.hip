@@ -360,6 +360,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   __shared__ ShadeLds cl;
   constexpr uint32_t RRT_SLOTS = SlotWindow<LEAN>::n;
   constexpr uint32_t STRIPE = RRT_STRIPE_OF(LEAN);
+  // the claim space (a multiple of 64 pixels: tiles of 8k x 8k) must hold whole stripes
+  static_assert(STRIPE > 0 && 64u % STRIPE == 0, "RRT_STRIPE must divide 64");
   __shared__ GroupLds<RRT_SLOTS> gs;
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
   float* const fg = cl.cg;

@@ -86,13 +86,13 @@ class Stats(C.Structure):
                 ("max_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("grid_n", C.c_uint32 * 3),
                 ("n_clean", C.c_uint32), ("n_big", C.c_uint32),
                 ("grid_free_frac", C.c_float), ("last_kernel_ms", C.c_float), ("grid_blocks", C.c_uint32),
-                ("block_threads", C.c_uint32), ("kernel", C.c_char * 64)]
+                ("block_threads", C.c_uint32), ("kernel", C.c_char * 64), ("last_main_kernel_ms", C.c_float)]
 
 
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)
 EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
            "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
-           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree",
+           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_launch_times", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree",
            "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load",
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
@@ -135,6 +135,7 @@ def lib():
         L.rrt_tonemap_device.argtypes = [vp, C.c_uint32, vp, vp, vp]
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.rrt_get_launch_times.argtypes = [vp, C.c_uint32, vp, vp]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
         for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_big_masks", 3),
                              ("rrt_get_occluders", 3)):
@@ -392,6 +393,14 @@ class Renderer:
         s = Stats()
         self._chk(lib().rrt_get_stats(self.h, C.byref(s)))
         return s
+
+    def launch_times(self, n):
+        """HIP-event ms of the last n (<= 32) launches, oldest first: (whole launch, main kernel)."""
+        tot, main = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        k = lib().rrt_get_launch_times(self.h, n, _p(tot), _p(main))
+        if k < 0:
+            self._chk(k)
+        return tot[:k], main[:k]
 
     def free_grid(self):
         """(k [nz][ny][nx] uint8, g0 (3,), inv_h, h_free) of the empty-space grid, or None."""

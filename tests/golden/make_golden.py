@@ -84,6 +84,22 @@ CASES = {
     "env_spheres_96x72_s8_hemi": ("CBspheres_lambertian.dae", ["-s", "8", "-H", "-r", "96", "72", "-e", "@sky"], True),
     "env_spheres_96x72_s32_l2": ("CBspheres_lambertian.dae", ["-s", "32", "-l", "2", "-r", "96", "72", "-e", "@sky"],
                                  True),
+    # the other light types (light.cpp:17-23 DirectionalLight, :34-42 InfiniteHemisphereLight):
+    # open scenes lit by a sun (teapot, cow) and by a sun plus an ambient sky (banana)
+    "teapot_64x48_s8": ("../meshedit/teapot.dae", ["-s", "8", "-r", "64", "48"], True),
+    "teapot_64x48_s8_m2": ("../meshedit/teapot.dae", ["-s", "8", "-m", "2", "-r", "64", "48"], True),
+    "cow_64x48_s8_m2": ("../meshedit/cow.dae", ["-s", "8", "-m", "2", "-r", "64", "48"], True),
+    "banana_64x48_s16": ("../keenan/banana.dae", ["-s", "16", "-r", "64", "48"], True),
+    "banana_64x48_s8_m2": ("../keenan/banana.dae", ["-s", "8", "-m", "2", "-r", "64", "48"], True),
+    "banana_64x48_s8_l4": ("../keenan/banana.dae", ["-s", "8", "-l", "4", "-r", "64", "48"], True),
+    # non-default -B (the proofs' envelope beyond the BASELINE framing; tools/proof_sweep.py):
+    # a larger hole with finer steps, a hole low in the room, a hole between camera and box
+    "bunny_B1_160x120_s16": ("CBbunny.dae", ["-s", "16", "-r", "160", "120", "-B", "0.3", "1.2", "-0.2", "0.25", "0.05"],
+                             True),
+    "spheres_B2_160x120_s16": ("CBspheres_lambertian.dae",
+                               ["-s", "16", "-r", "160", "120", "-B", "0", "0.5", "0", "0.4", "0.2"], True),
+    "bunny_B3_160x120_s16": ("CBbunny.dae", ["-s", "16", "-r", "160", "120", "-B", "0", "1", "1.5", "0.15", "0.08"],
+                             True),
 }
 # cases whose reference PNG outputs (save_image + save_sampling_rate_image, via -f) are kept as
 # ref.png / ref_rate.png, for the rrt_render CLI tests
@@ -129,6 +145,13 @@ def render(dae, args, workdir, threads, seed=0):
     return prefix
 
 
+def light_types(prefix):
+    """The flattened scene's light types (include/rrt.h RRT_LIGHT_*), from the reference's dump."""
+    sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
+    import rrt
+    return sorted({int(t) for t, _, _ in rrt.SceneFile(prefix + ".rrts").lights()})
+
+
 def load_px(prefix, counters):
     d = {k: np.load(f"{prefix}_px_{k}.npy") for k in ("rgb", "count", "draws", "meta")}
     if counters:
@@ -167,7 +190,7 @@ def main():
             # generated scenes are not stored (the tests regenerate them and check the digest)
             sdir = os.path.join(GOLD, "scenes") if dae not in GENERATED else os.path.join(td, "scenes")
             os.makedirs(sdir, exist_ok=True)
-            stem = dae.replace(".dae", "")
+            stem = os.path.basename(dae).replace(".dae", "")
             spath = os.path.join(sdir, stem + ".rrts")
             with open(prefix + ".rrts", "rb") as f:
                 sbytes = f.read()
@@ -187,10 +210,12 @@ def main():
                 shutil.copy(os.path.join(td, "out.png"), os.path.join(out, "ref.png"))
                 shutil.copy(os.path.join(td, "out_rate.png"), os.path.join(out, "ref_rate.png"))
             px = load_px(prefix, counters)
+            lt = light_types(prefix)
             np.savez_compressed(os.path.join(out, "px.npz"), **px)
         meta = px["meta"]
         info = {
-            "dae": dae, "scene": dae if dae in GENERATED else "scenes/" + dae.replace(".dae", "") + ".rrts",
+            "dae": dae, "scene": dae if dae in GENERATED else "scenes/" + os.path.basename(dae).replace(".dae", "") + ".rrts",
+            "light_types": lt,
             "args": args,
             "seed": 0, "threads": a.jobs,
             "region": {"x0": int(meta[0]), "y0": int(meta[1]), "w": int(meta[2]), "h": int(meta[3])},

@@ -69,6 +69,8 @@ def lib():
                                      C.POINTER(C.c_int), _f32p]
         L.ro_area_sample.argtypes = [_f32p, _f64p, _f64p, _i32p, _f32p, _f64p, C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]
+        L.ro_light_sample.argtypes = [C.c_int, _f32p, _f64p, _f64p, _i32p, _f32p, _f64p, C.POINTER(C.c_float),
+                                      C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.ro_camera_ray.argtypes = [C.c_double, C.c_double, _f64p, _f64p, C.c_double, C.c_double, C.c_double,
                                     C.c_double, _f64p, _f64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.ro_scene_set_envmap.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]

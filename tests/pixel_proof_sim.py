@@ -80,10 +80,8 @@ def prove(K, O, dc, corners):
         for k in range(4):
             w = v[1] + (dv if k & 1 else -dv)
             wp = vp[1] + (dvp if k & 2 else -dvp)
-            awp = abs(wp)
-            D = w * w + wp * wp - 2.0 * K["co1"] * awp * w
-            inside = w * (K["co1"] * awp - w) < 0.0 and awp * (awp - K["co1"] * w) > 0.0
-            far = far and (si2 > rb * rb * D if inside else rho * rho > rb * rb * max(w * w, wp * wp))
+            D = w * w + wp * wp - 2.0 * K["co1"] * abs(wp) * w
+            far = far and si2 > rb * rb * D  # the line distance, a lower bound on the segment's
         if not far:
             pa = O if j == 0 else c + (ea * rho / vp[1]) * X + (eb * rho / vp[1]) * Yc
             pb = c + (na * rho / v[1]) * X + (nb * rho / v[1]) * Yc

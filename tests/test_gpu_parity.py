@@ -45,7 +45,11 @@ def check(c, rgb, cnt, draws):
         if draws is not None:
             assert np.array_equal(draws, c.px["draws"])
     else:
+        # north star: per-pixel L2 <= 1e-4.  A device-libm ulp in a transcendental can flip one
+        # sample's branch (a bounce, a coin flip) and move that pixel by more; such outliers stay
+        # rare (<= 1% of pixels) and the RMS over all and over lit pixels stays within tolerance
         assert m["rms"] <= TOL and m["rms_nonblack"] <= TOL, m
+        assert m["over_tol_frac"] <= 0.01, m
         assert np.mean(cnt == c.px["count"]) > 0.99
     return m
 

@@ -81,7 +81,7 @@ def test_camera_placement_per_render_case(case):
         path = os.path.join(tempfile.mkdtemp(), "gen.dae")
         assert {"@cfg4": rrt_scenes.write_cfg4_dae}[c["dae"]](path) == c["dae_sha256"]
     else:
-        path = _input(c["dae"][:-4])
+        path = _input(os.path.basename(c["dae"])[:-4])
     _, cam = rrt.load_collada(path, w, h, lr, fd)
     ref = rrt.load_camera_state(os.path.join(GOLD, case, "camera.rrtc"))
     assert bytes(cam) == bytes(ref)

@@ -137,6 +137,31 @@ def test_area_light():
         assert np.float32(pdf.value) == np.float32(r[27])
 
 
+def test_point_directional_hemisphere_lights():
+    """PointLight / DirectionalLight / InfiniteHemisphereLight::sample_L (light.cpp:17-23, 34-42,
+    49-57) with scripted draws; the light's own vector comes from the reference object (the
+    ingest's construction of it is pinned by tests/test_ingest.py)."""
+    v = kat("light")
+    hemi_frame = np.array([[1, 0, 0], [0, 0, -1], [0, 1, 0], [0, 0, 0]], np.float64)  # light.cpp:29-31
+    for r in v:
+        kind = int(r[0])
+        vv = hemi_frame.copy() if kind == 3 else np.zeros((4, 3))
+        if kind != 3:
+            vv[0] = r[7:10]
+        L = np.zeros(3, np.float32)
+        wi = np.zeros(3)
+        dist, pdf, used = C.c_float(), C.c_float(), C.c_int()
+        O.lib().ro_light_sample(kind, r[1:4].astype(np.float32), np.ascontiguousarray(vv.ravel()),
+                                np.ascontiguousarray(r[10:13]), np.array(r[13:15], np.int32), L, wi,
+                                C.byref(dist), C.byref(pdf), C.byref(used))
+        assert np.array_equal(L, r[15:18].astype(np.float32)), r
+        assert same(wi, r[18:21]), (kind, wi, r[18:21])
+        assert np.float32(dist.value) == np.float32(r[21]) or (np.isinf(dist.value) and np.isinf(r[21]))
+        assert np.float32(pdf.value) == np.float32(r[22])
+        assert used.value == int(r[23])
+    assert {int(k) for k in v[:, 0]} == {1, 2, 3}
+
+
 def test_camera_ray():
     v = kat("camray")
     for r in v:

@@ -52,6 +52,21 @@ for step in "$@"; do
     prof5) run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline ;;
     diag)  run diag 600 python3 tools/diag_clear.py --res 64 128 192 256 ;;
     ab)    run ab 900 python3 tools/ab_kernels.py --rounds ${AB_ROUNDS:-3} ${AB_VARIANTS:-lean1:0:1 lean2:0:2 lean3:0:3 lean4:0:4 mega2:4:2} ;;
+    avail) run avail 120 rocprofv3 --list-avail ;;
+    ubench) run ubench_f64 300 ./tools/ubench_f64 ;;
+    crop)  # the cfg3 lit streak alone on an idle GPU: the per-pixel latency floor of the frame's tail
+           run crop_streak 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0 &&
+           run crop_tiles 300 python3 tools/crop_probe.py --region 960 576 32 64 --no-counters --flags 0 ;;
+    valu)  # PMC passes over the bench's launches (-> tools/pmc_valu.py): FP64 VALU mix, lane utilisation,
+           # clock; HBM fetch / write.  One rocprofv3 run per pass.
+           W=${PMC_WORKLOAD:-cfg3}; K=${PMC_KERNEL:-rrt_batch_kernel<1, 5>}
+           run pmc_valu_$W 600 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmcv_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
+           run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmcf_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
+           run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmcw_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
+           run pmc_json_$W 60 python3 tools/pmc_valu.py gpurun_out/pmcv_$W gpurun_out/pmcf_$W gpurun_out/pmcw_$W --workload $W --kernel "$K" --out gpurun_out/r03_${W}_pmc.json ;;
+    cropw) # the streak crop at 2..5 waves/SIMD (register budget vs spills) and its phase profile
+           run cropw 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0:2 0:3 0:4 0:5 &&
+           RRT_LIB=tools/_var/librrt_prof.so run crop_phase 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
