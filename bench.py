@@ -33,8 +33,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "relativistic-ray-tracer_amd"))
-# rrt / rrt_frame (librrt.so) are imported in main(), after the rank launcher: the parent of a
-# multi-rank run must not load the HIP library or touch the GPU before its ranks start
+# importing rrt does not load librrt.so (rrt.lib() does, on first use): the parent of a
+# multi-rank run loads no HIP library and touches no GPU before its ranks start
+import rrt  # noqa: E402
+import rrt_frame  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
@@ -273,9 +275,6 @@ def main():
     if mode == "launch":
         sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
 
-    global rrt, rrt_frame
-    import rrt
-    import rrt_frame
     import torch
     import torch.distributed as dist
 

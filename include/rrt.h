@@ -122,6 +122,14 @@ typedef struct {
  * RRT_METRIC_KERR swaps BlackHole::next_micro_ray for an RK4 null-geodesic step in Kerr-Schild
  * coordinates; the rest of BVHAccel::intersect (segment tests, capture = no hit) is unchanged. */
 int rrt_set_spacetime(rrt_ctx* ctx, const rrt_spacetime_desc* st);
+/* The validated envelope of the camera / pixel / shadow proofs (profiles/
+ * r03_proof_sweep.json): delta_theta in [RRT_PROOF_DT_MIN, RRT_PROOF_DT_MAX] and r_s <=
+ * RRT_PROOF_RS_OVER_EXTENT x the scene's largest root-box extent.  Outside it the kernels march
+ * every ray exactly.  Returns 1 if the context's scene and Schwarzschild hole are inside it. */
+#define RRT_PROOF_DT_MIN 0.04
+#define RRT_PROOF_DT_MAX 0.6
+#define RRT_PROOF_RS_OVER_EXTENT 0.5
+int rrt_proof_envelope(const rrt_ctx* ctx);
 /* The Kerr local frame for a spin axis (ez = unit(axis), ex, ey completing a right-handed
  * basis), so a checker can restate the integrator in the same coordinates. */
 void rrt_kerr_frame(const double* axis3, double* ex3, double* ey3, double* ez3);
@@ -190,6 +198,10 @@ enum {
   RRT_RENDER_NO_SHADOW_PROOF = 1u << 16, /* march every shadow ray exactly instead of first trying
                                      the occlusion proof (a certain crossing of a root-box face
                                      triangle before any possible capture; A/B and parity) */
+  RRT_RENDER_NO_SEARCH_TREE = 1u << 18, /* walk the clean tree (left-first, the reference's order)
+                                     instead of the SAH search tree over the same leaves with the
+                                     ordered replay of accepted primitives (A/B; results are
+                                     identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of
@@ -266,6 +278,10 @@ int rrt_get_bvh(const rrt_ctx* ctx, double* boxes, int32_t* nodes, uint32_t* pri
  * big_boxes [nb][6], big [nb][3] = (first slot, slot count, ordinal).  Returns n (0 = none);
  * query nb through rrt_get_stats.  Any pointer may be NULL. */
 int rrt_get_clean_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes, double* big_boxes, int32_t* big);
+/* The search tree: an SAH hierarchy over the clean tree's leaves in pre-order,
+ * boxes [n][6], nodes [n][4] = (skip, first slot, slot count (0 = inner), the leaf's left-first
+ * ordinal).  Returns n (0 = none); call with NULL pointers to get n. */
+int rrt_get_search_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes);
 
 /* The empty-space grid: k [n[2]][n[1]][n[0]] uint8 Chebyshev cell distances,
  * geom = {g0.x, g0.y, g0.z, 1/h, h_free}.  Returns the number of cells (0 = no grid); any

@@ -485,50 +485,46 @@ static inline ray_t next_micro_ray(const hole_t* h, const ray_t* ray) {
  *   l = (1, (r x + a y) / (r^2 + a^2), (r y - a x) / (r^2 + a^2), z / r),
  *   r^2 = (rho^2 - a^2) / 2 + sqrt((rho^2 - a^2)^2 / 4 + a^2 z^2).
  * H = (|p|^2 - f L^2) / 2 with p_t = -1, L = 1 + l . p:
- *   dq/dl = p - f L l,  dp/dl = (1/2) grad(f L^2)   (gradient by forward-mode duals). */
-typedef struct { double v, x, y, z; } dn;
-static inline dn DN(double v, double x, double y, double z) { dn r = {v, x, y, z}; return r; }
-static inline dn dadd(dn a, dn b) { return DN(a.v + b.v, a.x + b.x, a.y + b.y, a.z + b.z); }
-static inline dn dsub(dn a, dn b) { return DN(a.v - b.v, a.x - b.x, a.y - b.y, a.z - b.z); }
-static inline dn dmul(dn a, dn b) {
-  return DN(a.v * b.v, a.x * b.v + a.v * b.x, a.y * b.v + a.v * b.y, a.z * b.v + a.v * b.z);
-}
-static inline dn dscale(double c, dn a) { return DN(c * a.v, c * a.x, c * a.y, c * a.z); }
-static inline dn ddiv(dn a, dn b) {
-  const double ib = 1.0 / b.v, q = a.v * ib;
-  return DN(q, (a.x - q * b.x) * ib, (a.y - q * b.y) * ib, (a.z - q * b.z) * ib);
-}
-static inline dn dsqrt(dn a) {
-  const double s = sqrt(a.v), k = 0.5 / s;
-  return DN(s, a.x * k, a.y * k, a.z * k);
-}
+ *   dq/dl = p - f L l,  dp/dl = (1/2) grad(f L^2) = L ((L/2) grad f + f grad L), the gradients in
+ * closed form: with Sigma = r^4 + a^2 z^2 and W = r^2 + a^2 (from r^4 - (rho^2 - a^2) r^2 - a^2 z^2 = 0),
+ *   grad r = (x r^3, y r^3, z r W) / Sigma,  grad f = f (3 grad r / r - (4 r^3 grad r + 2 a^2 z e_z) / Sigma),
+ *   grad l_x = (r e_x + a e_y) / W + (x - 2 r l_x) grad r / W,  grad l_y = (r e_y - a e_x) / W + (y - 2 r l_y) grad r / W,
+ *   grad l_z = e_z / r - z grad r / r^2. */
 static inline double kerr_r2(const hole_t* h, v3 q) {
   const double w = ((q.x * q.x + q.y * q.y) + q.z * q.z) - h->a2;
   return 0.5 * w + sqrt(0.25 * (w * w) + h->a2 * (q.z * q.z));
 }
-static inline void kerr_fl(const hole_t* h, v3 q, dn* f, dn* lx, dn* ly, dn* lz, double* r_out) {
-  const dn X = DN(q.x, 1, 0, 0), Y = DN(q.y, 0, 1, 0), Z = DN(q.z, 0, 0, 1);
-  const dn zz = dmul(Z, Z);
-  const dn w = DN(((q.x * q.x + q.y * q.y) + q.z * q.z) - h->a2, 2 * q.x, 2 * q.y, 2 * q.z);
-  const dn disc = dadd(dscale(0.25, dmul(w, w)), dscale(h->a2, zz));
-  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc));
-  const dn r = dsqrt(r2);
-  const dn den = DN(r2.v + h->a2, r2.x, r2.y, r2.z);
-  *lx = ddiv(dadd(dmul(r, X), dscale(h->a, Y)), den);
-  *ly = ddiv(dsub(dmul(r, Y), dscale(h->a, X)), den);
-  *lz = ddiv(Z, r);
-  const dn r4 = dmul(r2, r2);
-  *f = ddiv(dscale(2.0 * h->m, dmul(r, r2)), dadd(r4, dscale(h->a2, zz)));
-  *r_out = r.v;
+/* values only: f, l, r at local point q */
+static inline void kerr_fl(const hole_t* h, v3 q, double* f, v3* l, double* r_out) {
+  const double zz = q.z * q.z;
+  const double w = ((q.x * q.x + q.y * q.y) + zz) - h->a2;
+  const double r2 = 0.5 * w + sqrt(0.25 * (w * w) + h->a2 * zz);
+  const double r = sqrt(r2);
+  const double iw = 1.0 / (r2 + h->a2);
+  *l = V((r * q.x + h->a * q.y) * iw, (r * q.y - h->a * q.x) * iw, q.z / r);
+  *f = ((2.0 * h->m) * (r * r2)) / (r2 * r2 + h->a2 * zz);
+  *r_out = r;
 }
-static inline void kerr_rhs(const hole_t* h, v3 q, v3 p, v3* dq, v3* dp, double* r) {
-  dn f, lx, ly, lz;
-  kerr_fl(h, q, &f, &lx, &ly, &lz, r);
-  const dn L = dadd(dadd(dadd(DN(1.0, 0, 0, 0), dscale(p.x, lx)), dscale(p.y, ly)), dscale(p.z, lz));
-  const dn F = dmul(f, dmul(L, L));
-  const double fL = f.v * L.v;
-  *dq = V(p.x - fL * lx.v, p.y - fL * ly.v, p.z - fL * lz.v);
-  *dp = V(0.5 * F.x, 0.5 * F.y, 0.5 * F.z);
+static inline void kerr_rhs(const hole_t* h, v3 q, v3 p, v3* dq, v3* dp, double* r_out) {
+  const double zz = q.z * q.z;
+  const double w = ((q.x * q.x + q.y * q.y) + zz) - h->a2;
+  const double r2 = 0.5 * w + sqrt(0.25 * (w * w) + h->a2 * zz);
+  const double r = sqrt(r2);
+  const double W = r2 + h->a2;
+  const double isg = 1.0 / (r2 * r2 + h->a2 * zz), iw = 1.0 / W, ir = 1.0 / r;
+  const double r3 = r * r2, gk = r3 * isg;
+  const v3 g = V(q.x * gk, q.y * gk, (q.z * r) * (W * isg));
+  const double lx = (r * q.x + h->a * q.y) * iw, ly = (r * q.y - h->a * q.x) * iw, lz = q.z * ir;
+  const double f = (2.0 * h->m) * gk;
+  const double cf = 3.0 * ir - (4.0 * r3) * isg;
+  const v3 gf = V(f * (cf * g.x), f * (cf * g.y), f * (cf * g.z - ((2.0 * h->a2) * q.z) * isg));
+  const double L = ((1.0 + p.x * lx) + p.y * ly) + p.z * lz;
+  const double c = (p.x * (q.x - (2.0 * r) * lx) + p.y * (q.y - (2.0 * r) * ly)) * iw - (p.z * q.z) * (ir * ir);
+  const v3 gL = V((r * p.x - h->a * p.y) * iw + c * g.x, (h->a * p.x + r * p.y) * iw + c * g.y, p.z * ir + c * g.z);
+  const double hL = 0.5 * L, fL = f * L;
+  *dq = V(p.x - fL * lx, p.y - fL * ly, p.z - fL * lz);
+  *dp = V(L * (hL * gf.x + f * gL.x), L * (hL * gf.y + f * gL.y), L * (hL * gf.z + f * gL.z));
+  *r_out = r;
 }
 static inline v3 kerr_local(const hole_t* h, v3 v) { return V(vdot(v, h->ex), vdot(v, h->ey), vdot(v, h->ez)); }
 static inline v3 kerr_world(const hole_t* h, v3 q) {
@@ -540,30 +536,33 @@ static inline v3 kerr_world(const hole_t* h, v3 q) {
 static inline void kerr_init(const hole_t* h, v3 o, v3 d, v3* q, v3* p) {
   *q = kerr_local(h, vsub(o, h->c));
   const v3 k = kerr_local(h, d);
-  dn f, lx, ly, lz;
-  double r;
-  kerr_fl(h, *q, &f, &lx, &ly, &lz, &r);
-  const double ld = (lx.v * k.x + ly.v * k.y) + lz.v * k.z;
-  const double A = f.v - 1.0, B = 2.0 * f.v * ld, C = 1.0 + f.v * (ld * ld);
+  double f, r;
+  v3 l;
+  kerr_fl(h, *q, &f, &l, &r);
+  const double ld = (l.x * k.x + l.y * k.y) + l.z * k.z;
+  const double A = f - 1.0, B = 2.0 * f * ld, C = 1.0 + f * (ld * ld);
   double disc = B * B - 4.0 * A * C;
   if (!(disc > 0.0)) disc = 0.0;
   const double kt = (2.0 * C) / (sqrt(disc) - B);
-  const double pt = A * kt + f.v * ld;
-  const double s = f.v * (kt + ld);
-  *p = V(k.x + s * lx.v, k.y + s * ly.v, k.z + s * lz.v);
+  const double pt = A * kt + f * ld;
+  const double s = f * (kt + ld);
+  *p = V(k.x + s * l.x, k.y + s * l.y, k.z + s * l.z);
   if (pt < 0.0) *p = vmul(*p, -1.0 / pt);
 }
 /* classical RK4 in the affine parameter from (q, p) with its first stage given, h = dtheta * r / |dq/dl| */
 static inline void kerr_step(const hole_t* h, v3* q, v3* p, v3 dq1, v3 dp1, double hh) {
-  v3 dq2, dp2, dq3, dp3, dq4, dp4;
+  v3 dq, dp, aq = dq1, ap = dp1;  /* running sums ((k1 + 2 k2) + 2 k3) + k4 */
   double rr;
   const double half = 0.5 * hh;
-  kerr_rhs(h, vadd(*q, vmul(dq1, half)), vadd(*p, vmul(dp1, half)), &dq2, &dp2, &rr);
-  kerr_rhs(h, vadd(*q, vmul(dq2, half)), vadd(*p, vmul(dp2, half)), &dq3, &dp3, &rr);
-  kerr_rhs(h, vadd(*q, vmul(dq3, hh)), vadd(*p, vmul(dp3, hh)), &dq4, &dp4, &rr);
+  kerr_rhs(h, vadd(*q, vmul(dq1, half)), vadd(*p, vmul(dp1, half)), &dq, &dp, &rr);
+  aq = vadd(aq, vmul(dq, 2.0)); ap = vadd(ap, vmul(dp, 2.0));
+  kerr_rhs(h, vadd(*q, vmul(dq, half)), vadd(*p, vmul(dp, half)), &dq, &dp, &rr);
+  aq = vadd(aq, vmul(dq, 2.0)); ap = vadd(ap, vmul(dp, 2.0));
+  kerr_rhs(h, vadd(*q, vmul(dq, hh)), vadd(*p, vmul(dp, hh)), &dq, &dp, &rr);
+  aq = vadd(aq, dq); ap = vadd(ap, dp);
   const double c6 = hh / 6.0;
-  *q = vadd(*q, vmul(vadd(vadd(vadd(dq1, vmul(dq2, 2.0)), vmul(dq3, 2.0)), dq4), c6));
-  *p = vadd(*p, vmul(vadd(vadd(vadd(dp1, vmul(dp2, 2.0)), vmul(dp3, 2.0)), dp4), c6));
+  *q = vadd(*q, vmul(aq, c6));
+  *p = vadd(*p, vmul(ap, c6));
 }
 /* one march step: 0 = stepped, 1 = escaped (outgoing beyond r_esc); *swept += polar angle */
 static inline int kerr_advance(const hole_t* h, v3* q, v3* p, double* swept) {

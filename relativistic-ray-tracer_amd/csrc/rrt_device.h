@@ -161,9 +161,6 @@ __device__ __forceinline__ bool in_fast_range(double v) {
   const double a = fabs(v);
   return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
 }
-#ifndef RRT_WALK_PREFETCH
-#define RRT_WALK_PREFETCH 0  // 1: traverse_clean prefetches both successor nodes (A/B)
-#endif
 #ifndef RRT_SLAB_APPROX
 #define RRT_SLAB_APPROX 1  // 0: every fast slab test takes the Markstein quotients (A/B)
 #endif
@@ -375,79 +372,130 @@ __device__ __forceinline__ bool leaf_may_hit(const KParams& kp, int first, int c
   return any;
 }
 
-// The same result as traverse(), over the "clean" tree (rrt_host.cpp build_clean_tree).
-// Why it is the same: the slab test is monotone under box inclusion (every quotient
-// RN((m - o) / d) is monotone in m), so a leaf's box passing implies every ancestor's box passes
-// at the ancestor's (earlier, larger-or-equal) max_t.  Hence the reference tests a leaf's
-// primitives exactly when that leaf's own box passes with the max_t left by the leaves before it
-// in left-first order -- inner boxes only prune.  So any walk that offers every leaf whose box
-// could pass, in left-first order, to the exact leaf test gives the reference's answer.  The
-// clean tree is the reference tree without its few oversized leaves (Cornell-box walls and
-// lights, whose boxes span the room and inflate every ancestor), with inner boxes refit to what
-// is left; the oversized leaves are tested directly from a short list, merged in by their
-// left-first ordinal.  The reference's root test comes first, so rays outside the scene still
-// cost one box test.
-__device__ __forceinline__ int next_big_in(uint64_t m, int from, int nb) {  // next set bit >= from, or nb
+// next set bit >= from of the oversized-leaf mask (bit i = kp.big[i]), or nb
+__device__ __forceinline__ int next_big_in(uint64_t m, int from, int nb) {
   const uint64_t r = from < 64 ? (m >> from) : 0ull;
   return r ? min(from + (int)__builtin_ctzll(r), nb) : nb;
 }
-// bmask: the oversized leaves the walk must offer (bit i = kp.big[i]; the others have no
-// primitive within reach of the segment, rrt_host.cpp build_big_masks)
+// BVHAccel::intersect_micro's result (bvh.cpp:115-138) from the search tree (rrt_host.cpp
+// build_free_tree): an SAH hierarchy over the reference tree's leaves -- their boxes and slot runs
+// are the reference's own -- without the oversized ones (the room's walls and lights, kp.big,
+// tested from a short list).  Why only leaf boxes matter: the slab test is monotone under box
+// inclusion (every quotient RN((m - o) / d) is monotone in m), so a passing leaf passes the
+// inner boxes above it, in any hierarchy; inner boxes only prune.
+// 1. Walk the search tree at the segment's full max_t L, in its own order, testing every leaf
+//    whose box passes (plus the oversized leaves): exactly the leaves whose boxes pass at L, the
+//    only ones the reference can test (max_t only shrinks and the slab test is monotone in it).
+//    No primitive accepted at L  <=>  the reference finds no hit (order plays no part): done.
+//    A shadow query (ANY) stops at the first accepted primitive, as before.
+// 2. A closest-hit query keeps the slots of the primitives accepted at L (at most 4; more: the
+//    clean walk instead) with their leaves, and replays the reference on them in slot order --
+//    slots are laid out in left-first leaf order, so slot order is the reference's visiting order:
+//    a leaf's box is tested once, with the max_t the reference would hold on reaching it, and its
+//    accepted primitives re-tested with that max_t.  Every other primitive the reference tests is
+//    rejected at L, hence at any max_t <= L (acceptance is t in [0, max_t] plus tests that do not
+//    depend on max_t; a sphere returns the same t whenever it accepts), so it changes nothing.
+//    Leaves without an accepted primitive do not change max_t, so the replay's max_t at each
+//    accepted leaf is the reference's: the result (slot, t, barycentrics) is the reference's.
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool traverse_clean(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
-                                               double& hb1, double& hb2, Counters& cn, bool exact,
-                                               uint64_t bmask = ~0ull) {
+__device__ __forceinline__ bool traverse_free(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
+                                              double& hb1, double& hb2, Counters& cn, bool exact,
+                                              uint64_t bmask = ~0ull) {
   if (COUNT) cn.bbox++;
   if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return false;
-  const v3 e = o + vmul(d, max_t);  // far end point (cull only; max_t only shrinks below)
-  bool hit = false;
+  const double L = max_t;
+  const v3 e = o + vmul(d, L);
   const int nb = (int)kp.n_big;
-  int bi = next_big_in(bmask, 0, nb);
-  int next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
-  int node = kp.clean_root;
-  // one item per iteration -- the next oversized leaf if it comes before the current node's
-  // subtree in left-first order, else the node -- so both kinds share one box test and one
-  // primitive loop (one set of temporaries)
+  bool hit = false;
+  double m = L;  // the reference's max_t as the replay goes
+  // Windows of the accepted primitives in slot order: each collect pass keeps the 4 smallest
+  // accepted slots above `after` (more than 4 on one segment take another pass); a leaf cut by
+  // the window edge keeps its box outcome for the next window
+  int32_t after = -1, leaf_cut = 0x7fffffff;
+  bool cut_pass = false;
+#pragma unroll 1
   for (;;) {
-    const bool more = node >= 0;
-    const DNode* n = more ? &kp.clean_nodes[node] : nullptr;
-    const bool big = next_big < (more ? n->pad : 0x7fffffff);
-    if (!big && !more) break;
-#if RRT_WALK_PREFETCH
-    // warm the cache lines of both possible next nodes (node + 1, the left child, after a passing
-    // inner box; skip otherwise) while this box is tested: the walk is a chain of dependent node
-    // loads.  The values are consumed only at the end of the iteration.
-    uint32_t w0 = 0u, w1 = 0u;
-    if (more && !big) {
-      if (n->count == 0) w0 = *(const volatile uint32_t*)&kp.clean_nodes[node + 1];
-      if (n->skip >= 0) w1 = *(const volatile uint32_t*)&kp.clean_nodes[n->skip];
+    int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+    int na = 0;
+    bool more = false;
+    // ---- collect: every leaf whose box passes at L -- the oversized leaves (the room's walls
+    // and lights: plane cull first, their boxes pass for almost every segment), then the search
+    // tree -- one item per iteration, so both kinds share one box test and one primitive loop
+    int bi = next_big_in(bmask, 0, nb), node = 0;
+#pragma unroll 1
+    for (;;) {
+      const bool big = bi < nb;
+      if (!big && node < 0) break;
+      const DNode* n = big ? nullptr : &kp.free_nodes[node];
+      const double* mn = big ? kp.big[bi].mn : n->mn;
+      const double* mx = big ? kp.big[bi].mx : n->mx;
+      const int first = big ? kp.big[bi].first : n->first;
+      const int count = big ? kp.big[bi].count : n->count;
+      bool pass = !big || leaf_may_hit<COUNT>(kp, first, count, o, e, cn);
+      if (pass) {
+        if (COUNT) cn.bbox++;
+        pass = slab_rt(mn, mx, o, d, y, L, exact);
+      }
+      if (pass && count != 0) {
+        const int32_t ref = big ? -1 - bi : node;
+#pragma unroll 1
+        for (int i = 0; i < count; ++i) {
+          const int32_t slot = first + i;
+          if (slot <= after) continue;
+          if (COUNT) cn.query++;
+          if (!plane_may_hit(kp.planes[slot], o, e, kp.plane_eps)) continue;
+          if (COUNT) cn.prim++;
+          const DPrimMeta meta = kp.meta[slot];
+          const DPrimGeo gp = kp.geo[slot];
+          double t, b1 = 0, b2 = 0;
+          const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, L, t)
+                                      : tri_t(gp, o, d, L, t, b1, b2);
+          if (!ok) continue;
+          if (ANY) return true;
+          if (na == 4) {  // keep the 4 smallest
+            more = true;
+            if (slot > s3) continue;
+            --na;
+          }
+          // insert keeping s0 < s1 < s2 < s3 (slots are distinct): shift the larger ones up
+          bool placed = false;
+          if (na >= 3) { if (s2 > slot) { s3 = s2; r3 = r2; } else { s3 = slot; r3 = ref; placed = true; } }
+          if (!placed && na >= 2) { if (s1 > slot) { s2 = s1; r2 = r1; } else { s2 = slot; r2 = ref; placed = true; } }
+          if (!placed && na >= 1) { if (s0 > slot) { s1 = s0; r1 = r0; } else { s1 = slot; r1 = ref; placed = true; } }
+          if (!placed) { s0 = slot; r0 = ref; }
+          ++na;
+        }
+      }
+      if (big) bi = next_big_in(bmask, bi + 1, nb);
+      else node = (pass && count == 0) ? node + 1 : n->skip;
     }
-#endif
-    const double* mn = big ? kp.big[bi].mn : n->mn;
-    const double* mx = big ? kp.big[bi].mx : n->mx;
-    const int first = big ? kp.big[bi].first : n->first;
-    const int count = big ? kp.big[bi].count : n->count;
-    // an oversized leaf's box (the room) passes for almost every segment: cull its primitives
-    // by their planes first and skip the box test when none survives
-    bool pass = !big || leaf_may_hit<COUNT>(kp, first, count, o, e, cn);
-    if (pass) {
-      if (COUNT) cn.bbox++;
-      pass = slab_rt(mn, mx, o, d, y, max_t, exact);
+    if (ANY || na == 0) break;
+    // ---- replay the reference on this window, in slot (= its visiting) order: a leaf's box is
+    // tested once, with the max_t held on reaching it
+    bool pass = false;
+    int32_t cur = 0x7fffffff;
+#pragma unroll 1
+    for (int k = 0; k < na; ++k) {
+      const int32_t slot = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+      const int32_t ref = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r3;
+      if (ref != cur) {
+        cur = ref;
+        const double* mn = ref >= 0 ? kp.free_nodes[ref].mn : kp.big[-1 - ref].mn;
+        const double* mx = ref >= 0 ? kp.free_nodes[ref].mx : kp.big[-1 - ref].mx;
+        pass = ref == leaf_cut ? cut_pass : slab_rt(mn, mx, o, d, y, m, exact);
+      }
+      if (!pass) continue;
+      const DPrimMeta meta = kp.meta[slot];
+      const DPrimGeo gp = kp.geo[slot];
+      double t, b1 = 0, b2 = 0;
+      const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, m, t)
+                                  : tri_t(gp, o, d, m, t, b1, b2);
+      if (ok) { m = t; hit = true; hit_slot = slot; hb1 = b1; hb2 = b2; }
     }
-    if (pass && count != 0 && leaf_prims_cull<ANY, COUNT>(kp, first, count, o, d, e, max_t, hit_slot, hb1, hb2, cn)) {
-      hit = true;
-      if (ANY) return true;
-    }
-#if RRT_WALK_PREFETCH
-    asm volatile("" ::"v"(w0), "v"(w1));
-#endif
-    if (big) {
-      bi = next_big_in(bmask, bi + 1, nb);
-      next_big = bi < nb ? kp.big[bi].dfs : 0x7fffffff;
-    } else {
-      node = (pass && count == 0) ? node + 1 : n->skip;
-    }
+    if (!more) break;
+    after = s3; leaf_cut = r3; cut_pass = pass;
   }
+  max_t = m;
   return hit;
 }
 
@@ -567,10 +615,10 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   const bool fast = segment_fast(kp, o, d);
   RRT_T0(tt0);
   bool hit;
-  if (!COUNT)  // the clean tree, or the reference tree itself with no oversized list (host)
-    hit = traverse_clean<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
+  if (!COUNT)  // the search tree (or, for A/B, the clean tree or the reference tree itself)
+    hit = traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
   else if (kp.count_exec)
-    hit = traverse_clean<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
+    hit = traverse_free<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
   else
     hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
@@ -616,10 +664,9 @@ __host__ __device__ constexpr int general_of(int v) { return v == V_KERR ? V_KER
 //   r^2 = (rho^2 - a^2) / 2 + sqrt((rho^2 - a^2)^2 / 4 + a^2 z^2)   (Boyer-Lindquist r).
 // Photons follow H = (eta^mn p_m p_n - f (l^m p_m)^2) / 2 = 0 with p_t = -1 (E = 1):
 //   dx_i/dl = p_i - f L l_i,   dp_i/dl = (1/2) d_i (f L^2),   L = 1 + l . p.
-// The gradient d_i(f L^2) is carried by forward-mode duals (value + d/dx, d/dy, d/dz).  At
-// a = 0 the spatial coordinates are r times the unit direction, so the spatial path is the
-// Schwarzschild photon orbit u'' + u = 3 M u^2 that BlackHole::next_micro_ray steps.
-struct dn { double v, x, y, z; };
+// The gradient d_i(f L^2) is evaluated in closed form (kerr_rhs).  At a = 0 the spatial
+// coordinates are r times the unit direction, so the spatial path is the Schwarzschild photon
+// orbit u'' + u = 3 M u^2 that BlackHole::next_micro_ray steps.
 // Arithmetic of one Kerr step (next_micro_impl's scheme): FAST takes the bare sqrt / division
 // cores and records in `ok` whether every operand lay in their exact range (a +0 numerator is
 // exact too); the caller re-runs the step IEEE (FAST = false) when one did not.
@@ -637,55 +684,54 @@ struct KArith {
     return div_core(a, b);
   }
 };
-__device__ __forceinline__ dn DN(double v, double x, double y, double z) { dn r; r.v = v; r.x = x; r.y = y; r.z = z; return r; }
-__device__ __forceinline__ dn dadd(dn a, dn b) { return DN(a.v + b.v, a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ dn dsub(dn a, dn b) { return DN(a.v - b.v, a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ dn dmul(dn a, dn b) {
-  return DN(a.v * b.v, a.x * b.v + a.v * b.x, a.y * b.v + a.v * b.y, a.z * b.v + a.v * b.z);
-}
-__device__ __forceinline__ dn dscale(double c, dn a) { return DN(c * a.v, c * a.x, c * a.y, c * a.z); }
+// Field quantities at local point q (values only: the capture test and the initial covector):
+// r (Boyer-Lindquist), f and l_i
 template <class A>
-__device__ __forceinline__ dn ddiv(dn a, dn b, A& ar) {  // q = a / b, q' = (a' - q b') / b, one division
-  const double ib = ar.dv(1.0, b.v), q = a.v * ib;
-  return DN(q, (a.x - q * b.x) * ib, (a.y - q * b.y) * ib, (a.z - q * b.z) * ib);
+__device__ __forceinline__ void kerr_fl(const DHole& h, v3 q, double& f, v3& l, double& r_out, A& ar) {
+  const double zz = q.z * q.z;
+  const double w = ((q.x * q.x + q.y * q.y) + zz) - h.a2;
+  const double r2 = 0.5 * w + ar.sq(0.25 * (w * w) + h.a2 * zz);
+  const double r = ar.sq(r2);
+  const double iw = ar.dv(1.0, r2 + h.a2);
+  l = V((r * q.x + h.a * q.y) * iw, (r * q.y - h.a * q.x) * iw, ar.dv(q.z, r));
+  f = ar.dv((2.0 * h.m) * (r * r2), r2 * r2 + h.a2 * zz);
+  r_out = r;
 }
-template <class A>
-__device__ __forceinline__ dn dsqrt(dn a, A& ar) {
-  const double s = ar.sq(a.v), k = ar.dv(0.5, s);
-  return DN(s, a.x * k, a.y * k, a.z * k);
-}
-// r^2 (Boyer-Lindquist) at local point q, values only (capture test)
+// r^2 (Boyer-Lindquist) at local point q (capture test)
 __device__ __forceinline__ double kerr_r2(const DHole& h, v3 q) {
   const double w = ((q.x * q.x + q.y * q.y) + q.z * q.z) - h.a2;
   return 0.5 * w + xsqrt(0.25 * (w * w) + h.a2 * (q.z * q.z));
 }
-// f and l_i at q, with gradients; r (value) out
+// Hamilton's equations at (q, p): dq = p - f L l, dp = (1/2) grad(f L^2) = L ((L/2) grad f + f grad L),
+// grad L = sum_i p_i grad l_i, with the gradients in closed form.  From the quartic
+// r^4 - (rho^2 - a^2) r^2 - a^2 z^2 = 0, with Sigma = r^4 + a^2 z^2 and W = r^2 + a^2:
+//   grad r = (x r^3, y r^3, z r W) / Sigma,
+//   grad f = f (3 grad r / r - (4 r^3 grad r + 2 a^2 z e_z) / Sigma)          (f = 2 M r^3 / Sigma),
+//   grad l_x = (r e_x + a e_y) / W + (x - 2 r l_x) grad r / W,
+//   grad l_y = (r e_y - a e_x) / W + (y - 2 r l_y) grad r / W,
+//   grad l_z = e_z / r - z grad r / r^2.
+// Three reciprocals and two square roots per evaluation; r out.
 template <class A>
-__device__ __forceinline__ void kerr_fl(const DHole& h, v3 q, dn& f, dn& lx, dn& ly, dn& lz, double& r_out, A& ar) {
-  const dn X = DN(q.x, 1, 0, 0), Y = DN(q.y, 0, 1, 0), Z = DN(q.z, 0, 0, 1);
-  const dn zz = dmul(Z, Z);
-  const dn w = DN(((q.x * q.x + q.y * q.y) + q.z * q.z) - h.a2, 2 * q.x, 2 * q.y, 2 * q.z);
-  const dn disc = dadd(dscale(0.25, dmul(w, w)), dscale(h.a2, zz));
-  const dn r2 = dadd(dscale(0.5, w), dsqrt(disc, ar));
-  const dn r = dsqrt(r2, ar);
-  const dn den = DN(r2.v + h.a2, r2.x, r2.y, r2.z);
-  lx = ddiv(dadd(dmul(r, X), dscale(h.a, Y)), den, ar);
-  ly = ddiv(dsub(dmul(r, Y), dscale(h.a, X)), den, ar);
-  lz = ddiv(Z, r, ar);
-  const dn r4 = dmul(r2, r2);
-  f = ddiv(dscale(2.0 * h.m, dmul(r, r2)), dadd(r4, dscale(h.a2, zz)), ar);
-  r_out = r.v;
-}
-// Hamilton's equations at (q, p): dq, dp; r out
-template <class A>
-__device__ __forceinline__ void kerr_rhs(const DHole& h, v3 q, v3 p, v3& dq, v3& dp, double& r, A& ar) {
-  dn f, lx, ly, lz;
-  kerr_fl(h, q, f, lx, ly, lz, r, ar);
-  const dn L = dadd(dadd(dadd(DN(1.0, 0, 0, 0), dscale(p.x, lx)), dscale(p.y, ly)), dscale(p.z, lz));
-  const dn F = dmul(f, dmul(L, L));
-  const double fL = f.v * L.v;
-  dq = V(p.x - fL * lx.v, p.y - fL * ly.v, p.z - fL * lz.v);
-  dp = V(0.5 * F.x, 0.5 * F.y, 0.5 * F.z);
+__device__ __forceinline__ void kerr_rhs(const DHole& h, v3 q, v3 p, v3& dq, v3& dp, double& r_out, A& ar) {
+  const double zz = q.z * q.z;
+  const double w = ((q.x * q.x + q.y * q.y) + zz) - h.a2;
+  const double r2 = 0.5 * w + ar.sq(0.25 * (w * w) + h.a2 * zz);
+  const double r = ar.sq(r2);
+  const double W = r2 + h.a2;
+  const double isg = ar.dv(1.0, r2 * r2 + h.a2 * zz), iw = ar.dv(1.0, W), ir = ar.dv(1.0, r);
+  const double r3 = r * r2, gk = r3 * isg;
+  const v3 g = V(q.x * gk, q.y * gk, (q.z * r) * (W * isg));  // grad r
+  const double lx = (r * q.x + h.a * q.y) * iw, ly = (r * q.y - h.a * q.x) * iw, lz = q.z * ir;
+  const double f = (2.0 * h.m) * gk;
+  const double cf = 3.0 * ir - (4.0 * r3) * isg;
+  const v3 gf = V(f * (cf * g.x), f * (cf * g.y), f * (cf * g.z - ((2.0 * h.a2) * q.z) * isg));
+  const double L = ((1.0 + p.x * lx) + p.y * ly) + p.z * lz;
+  const double c = (p.x * (q.x - (2.0 * r) * lx) + p.y * (q.y - (2.0 * r) * ly)) * iw - (p.z * q.z) * (ir * ir);
+  const v3 gL = V((r * p.x - h.a * p.y) * iw + c * g.x, (h.a * p.x + r * p.y) * iw + c * g.y, p.z * ir + c * g.z);
+  const double hL = 0.5 * L, fL = f * L;
+  dq = V(p.x - fL * lx, p.y - fL * ly, p.z - fL * lz);
+  dp = V(L * (hL * gf.x + f * gL.x), L * (hL * gf.y + f * gL.y), L * (hL * gf.z + f * gL.z));
+  r_out = r;
 }
 __device__ __forceinline__ v3 kerr_local(const DHole& h, v3 v) {
   return V(dot(v, ld3(h.ex)), dot(v, ld3(h.ey)), dot(v, ld3(h.ez)));
@@ -702,17 +748,17 @@ __device__ __forceinline__ void kerr_init(const DHole& h, v3 o, v3 d, v3& q, v3&
   KArith<false> ar;
   q = kerr_local(h, o - ld3(h.c));
   const v3 k = kerr_local(h, d);
-  dn f, lx, ly, lz;
-  double r;
-  kerr_fl(h, q, f, lx, ly, lz, r, ar);
-  const double ld = (lx.v * k.x + ly.v * k.y) + lz.v * k.z;
-  const double A = f.v - 1.0, B = 2.0 * f.v * ld, C = 1.0 + f.v * (ld * ld);
+  double f, r;
+  v3 l;
+  kerr_fl(h, q, f, l, r, ar);
+  const double ld = (l.x * k.x + l.y * k.y) + l.z * k.z;
+  const double A = f - 1.0, B = 2.0 * f * ld, C = 1.0 + f * (ld * ld);
   double disc = B * B - 4.0 * A * C;
   if (!(disc > 0.0)) disc = 0.0;
   const double kt = (2.0 * C) / (sqrt(disc) - B);
-  const double pt = A * kt + f.v * ld;
-  const double s = f.v * (kt + ld);
-  p = V(k.x + s * lx.v, k.y + s * ly.v, k.z + s * lz.v);
+  const double pt = A * kt + f * ld;
+  const double s = f * (kt + ld);
+  p = V(k.x + s * l.x, k.y + s * l.y, k.z + s * l.z);
   if (pt < 0.0) p = vmul(p, -1.0 / pt);
 }
 // One march step: the first RK4 stage at (q, p); escape test (outgoing beyond r_esc: returns
@@ -720,7 +766,7 @@ __device__ __forceinline__ void kerr_init(const DHole& h, v3 o, v3 d, v3& q, v3&
 // swept; then the classical RK4 update.
 template <class A>
 __device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, double& swept, A& ar) {
-  v3 dq1, dp1, dq2, dp2, dq3, dp3, dq4, dp4;
+  v3 dq1, dp1;
   double r, rr;
   kerr_rhs(h, q, p, dq1, dp1, r, ar);
   const double rho2 = norm2(q);
@@ -728,12 +774,18 @@ __device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, doubl
   const double hh = ar.dv(h.dt * r, ar.sq(norm2(dq1)));
   swept += ar.dv(hh * ar.sq(norm2(cross(q, dq1))), rho2);  // polar angle of this step
   const double half = 0.5 * hh;
-  kerr_rhs(h, q + vmul(dq1, half), p + vmul(dp1, half), dq2, dp2, rr, ar);
-  kerr_rhs(h, q + vmul(dq2, half), p + vmul(dp2, half), dq3, dp3, rr, ar);
-  kerr_rhs(h, q + vmul(dq3, hh), p + vmul(dp3, hh), dq4, dp4, rr, ar);
+  // stages 2-4 folded into running sums as they come: ((k1 + 2 k2) + 2 k3) + k4, the same
+  // operations in the same order as summing at the end, with one stage live at a time
+  v3 aq = dq1, ap = dp1, dq, dp;
+  kerr_rhs(h, q + vmul(dq1, half), p + vmul(dp1, half), dq, dp, rr, ar);
+  aq = aq + vmul(dq, 2.0); ap = ap + vmul(dp, 2.0);
+  kerr_rhs(h, q + vmul(dq, half), p + vmul(dp, half), dq, dp, rr, ar);
+  aq = aq + vmul(dq, 2.0); ap = ap + vmul(dp, 2.0);
+  kerr_rhs(h, q + vmul(dq, hh), p + vmul(dp, hh), dq, dp, rr, ar);
+  aq = aq + dq; ap = ap + dp;
   const double c6 = ar.dv(hh, 6.0);
-  q = q + vmul(((dq1 + vmul(dq2, 2.0)) + vmul(dq3, 2.0)) + dq4, c6);
-  p = p + vmul(((dp1 + vmul(dp2, 2.0)) + vmul(dp3, 2.0)) + dp4, c6);
+  q = q + vmul(aq, c6);
+  p = p + vmul(ap, c6);
   return false;
 }
 // BVHAccel::intersect with the Kerr march.  Like the reference's march it

@@ -138,6 +138,8 @@ struct rrt_ctx {
   std::vector<DNode> clean;  // host copies (rrt_get_clean_tree)
   std::vector<DBig> big;
   std::vector<uint32_t> big_mask;   // build_big_masks (host copy; rrt_get_big_masks)
+  std::vector<DNode> free_tree;     // build_free_tree: SAH hierarchy over the clean tree's leaves
+  DNode* d_free = nullptr;
   DShadowProof occ{};               // build_occluders (the root box's face triangles)
   uint32_t* d_big_mask = nullptr;
   uint64_t device_bytes = 0;
@@ -182,6 +184,8 @@ static void free_scene_dev(rrt_ctx* c) {
   hipFree(c->d_nodes); hipFree(c->d_geo); hipFree(c->d_nrm); hipFree(c->d_meta); hipFree(c->d_bsdfs);
   hipFree(c->d_lights); hipFree(c->d_grid); hipFree(c->d_clean); hipFree(c->d_big); hipFree(c->d_planes);
   hipFree(c->d_big_mask);
+  hipFree(c->d_free);
+  c->d_free = nullptr;
   c->d_grid = nullptr; c->d_clean = nullptr; c->d_big = nullptr; c->d_planes = nullptr; c->d_big_mask = nullptr;
   c->d_nodes = nullptr; c->d_geo = nullptr; c->d_nrm = nullptr; c->d_meta = nullptr; c->d_bsdfs = nullptr;
   c->d_lights = nullptr;
@@ -625,6 +629,102 @@ static void build_clean_tree(rrt_ctx* c, std::vector<DNode>& out, std::vector<DB
   c->has_clean = true; c->clean_root = 0; c->n_big = (uint32_t)big.size();
 }
 
+// Search tree for traverse_free (rrt_device.h): the clean tree's leaves -- the reference's own
+// leaf boxes and slot runs -- under a new binary hierarchy chosen by the surface-area heuristic
+// (full sweep over centroid-sorted leaves on each axis), in pre-order with skip pointers.  Inner
+// boxes are exact unions of their leaves' boxes, so the slab test's monotonicity under box
+// inclusion lets the walk prune with them; only the leaf boxes decide which primitives are
+// tested, exactly as in the reference ("search tree").  DNode.pad of a leaf: its
+// left-first ordinal.
+static void build_free_tree(rrt_ctx* c) {
+  c->free_tree.clear();
+  struct Item { double mn[3], mx[3], cen[3]; int32_t first, count, ord; };
+  std::vector<Item> items;
+  if (c->has_clean) {
+    for (const DNode& n : c->clean)
+      if (n.count != 0) {
+        Item it;
+        for (int k = 0; k < 3; ++k) { it.mn[k] = n.mn[k]; it.mx[k] = n.mx[k]; it.cen[k] = 0.5 * (n.mn[k] + n.mx[k]); }
+        it.first = n.first; it.count = n.count; it.ord = n.pad;
+        items.push_back(it);
+      }
+  } else {  // no oversized leaves: every reference leaf
+    int32_t ord = 0;
+    for (const BNode& n : c->nodes)
+      if (n.count != 0) {
+        Item it;
+        const double mn[3] = {n.bb.mn.x, n.bb.mn.y, n.bb.mn.z}, mx[3] = {n.bb.mx.x, n.bb.mx.y, n.bb.mx.z};
+        for (int k = 0; k < 3; ++k) { it.mn[k] = mn[k]; it.mx[k] = mx[k]; it.cen[k] = 0.5 * (mn[k] + mx[k]); }
+        it.first = n.first; it.count = n.count; it.ord = ord++;
+        items.push_back(it);
+      }
+  }
+  if (items.size() < 2) return;
+  auto area = [](const double* mn, const double* mx) {
+    const double ex = std::max(mx[0] - mn[0], 0.0), ey = std::max(mx[1] - mn[1], 0.0), ez = std::max(mx[2] - mn[2], 0.0);
+    return ex * ey + ey * ez + ez * ex;
+  };
+  std::vector<DNode>& out = c->free_tree;
+  out.reserve(2 * items.size());
+  std::vector<int32_t> idx(items.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+  std::vector<double> left_area;
+  // returns the node index; children laid out in pre-order (left = me + 1)
+  std::function<int32_t(int32_t*, int32_t)> rec = [&](int32_t* ids, int32_t n) -> int32_t {
+    const int32_t me = (int32_t)out.size();
+    out.push_back(DNode{});
+    DNode box{};
+    for (int k = 0; k < 3; ++k) { box.mn[k] = INFINITY; box.mx[k] = -INFINITY; }
+    for (int32_t i = 0; i < n; ++i)
+      for (int k = 0; k < 3; ++k) {
+        box.mn[k] = std::min(box.mn[k], items[ids[i]].mn[k]);
+        box.mx[k] = std::max(box.mx[k], items[ids[i]].mx[k]);
+      }
+    if (n == 1) {
+      const Item& it = items[ids[0]];
+      DNode& d = out[me];
+      for (int k = 0; k < 3; ++k) { d.mn[k] = it.mn[k]; d.mx[k] = it.mx[k]; }
+      d.first = it.first; d.count = it.count; d.pad = it.ord; d.skip = -1;
+      return me;
+    }
+    int best_axis = 0, best_k = n / 2;
+    double best = INFINITY;
+    left_area.resize(n);
+    for (int ax = 0; ax < 3; ++ax) {
+      std::stable_sort(ids, ids + n, [&](int32_t a, int32_t b) { return items[a].cen[ax] < items[b].cen[ax]; });
+      double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) { mn[k] = std::min(mn[k], items[ids[i]].mn[k]); mx[k] = std::max(mx[k], items[ids[i]].mx[k]); }
+        left_area[i] = area(mn, mx);
+      }
+      for (int k = 0; k < 3; ++k) { mn[k] = INFINITY; mx[k] = -INFINITY; }
+      for (int32_t i = n - 1; i >= 1; --i) {
+        for (int k = 0; k < 3; ++k) { mn[k] = std::min(mn[k], items[ids[i]].mn[k]); mx[k] = std::max(mx[k], items[ids[i]].mx[k]); }
+        const double cost = left_area[i - 1] * i + area(mn, mx) * (n - i);
+        if (cost < best) { best = cost; best_axis = ax; best_k = i; }
+      }
+    }
+    std::stable_sort(ids, ids + n, [&](int32_t a, int32_t b) { return items[a].cen[best_axis] < items[b].cen[best_axis]; });
+    rec(ids, best_k);
+    const int32_t r = rec(ids + best_k, n - best_k);
+    DNode& d = out[me];
+    d = box;
+    d.count = 0; d.first = 0; d.pad = 0; d.skip = -1;
+    (void)r;
+    return me;
+  };
+  rec(idx.data(), (int32_t)idx.size());
+  // skip pointers: the pre-order successor of each subtree
+  std::vector<int32_t> end(out.size());
+  std::function<int32_t(int32_t)> fill = [&](int32_t i) -> int32_t {
+    if (out[i].count != 0) return end[i] = i + 1;
+    const int32_t j = fill(i + 1);
+    return end[i] = fill(j);
+  };
+  fill(0);
+  for (size_t i = 0; i < out.size(); ++i) out[i].skip = end[i] < (int32_t)out.size() ? end[i] : -1;
+}
+
 static int upload(rrt_ctx* c, void** dst, const void* src, size_t bytes) {
   if (bytes == 0) bytes = 16;
   HIPCHK(c, hipMalloc(dst, bytes));
@@ -790,6 +890,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   build_free_grid(c);
   build_occluders(c);
   build_clean_tree(c, c->clean, c->big);
+  build_free_tree(c);
   build_big_masks(c);
   {  // plane-cull margin: 1e-9 of the scene's coordinate scale (rounding is ~1e-16 of it)
     const Box& rb = c->nodes[0].bb;
@@ -819,6 +920,9 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if ((rc = upload_lights(c))) return rc;
   if (!c->grid.empty() && (rc = upload(c, (void**)&c->d_grid, c->grid.data(), c->grid.size()))) return rc;
   if ((rc = upload(c, (void**)&c->d_planes, planes.data(), planes.size() * sizeof(DPlane)))) return rc;
+  if (!c->free_tree.empty() &&
+      (rc = upload(c, (void**)&c->d_free, c->free_tree.data(), c->free_tree.size() * sizeof(DNode))))
+    return rc;
   if (c->has_clean) {
     if ((rc = upload(c, (void**)&c->d_clean, c->clean.data(), c->clean.size() * sizeof(DNode)))) return rc;
     if ((rc = upload(c, (void**)&c->d_big, c->big.data(), c->big.size() * sizeof(DBig)))) return rc;
@@ -979,6 +1083,23 @@ static int scratch_release(rrt_ctx* c, hipStream_t stream) {
   return RRT_OK;
 }
 
+// The envelope the three proofs were validated in (tools/proof_sweep.py, profiles/
+// r03_proof_sweep.json: random holes inside and outside the room, cameras and resolutions, every
+// Cornell-box scene; the recurrence's deviation from the reference's march stayed >= 1000x below
+// the margins and no proven ray or pixel was contradicted): delta_theta in [0.04, 0.6] and r_s at
+// most half the root box's largest extent.  Outside it every ray is marched exactly.
+static bool in_proof_envelope(const rrt_ctx* c) {
+  if (!c->has_scene || c->hole.kind != RRT_METRIC_SCHWARZSCHILD) return false;
+  const Box& rb = c->nodes[0].bb;
+  const double ext = std::max(std::max(rb.mx.x - rb.mn.x, rb.mx.y - rb.mn.y), rb.mx.z - rb.mn.z);
+  return c->hole.dt >= RRT_PROOF_DT_MIN && c->hole.dt <= RRT_PROOF_DT_MAX && c->hole.r >= 0.0 &&
+         c->hole.r <= RRT_PROOF_RS_OVER_EXTENT * ext && std::isfinite(ext);
+}
+extern "C" int rrt_proof_envelope(const rrt_ctx* c) {
+  if (!c) return RRT_E_INVALID;
+  return in_proof_envelope(c) ? 1 : 0;
+}
+
 static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles, uint32_t ts,
                   uint32_t cx0, uint32_t cy0, uint32_t cx1, uint32_t cy1, float* d_rgb, int32_t* d_cnt,
                   uint32_t* d_draws, uint32_t* d_ctr, hipStream_t stream) {
@@ -1022,6 +1143,19 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.big = c->d_big; kp.clean_root = 0; kp.n_big = use_clean ? c->n_big : 0u;
   kp.big_mask = (use_clean && !(p->flags & RRT_RENDER_NO_SKIP)) ? c->d_big_mask : nullptr;
   kp.big_reach = (RRT_BIG_REACH - 1) * c->hgrid.h_free;
+  // the walk's hierarchy (rrt_device.h traverse_free): the SAH search tree by default; for A/B
+  // the clean tree (RRT_RENDER_NO_SEARCH_TREE) or the reference tree itself (RRT_RENDER_NO_CLEAN,
+  // no oversized list) -- every one of them holds the reference's leaves, so results are equal
+  {
+    const bool no_search = (p->flags & RRT_RENDER_NO_SEARCH_TREE) || !c->d_free;
+    if ((p->flags & RRT_RENDER_NO_CLEAN) || (!c->has_clean && no_search)) {
+      kp.free_nodes = c->d_nodes; kp.n_big = 0;
+    } else if (no_search) {
+      kp.free_nodes = c->d_clean;
+    } else {
+      kp.free_nodes = c->d_free;  // over the clean tree's leaves (+ kp.big), or every leaf
+    }
+  }
   kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
   {
     const Box& rb = c->nodes[0].bb;
@@ -1071,7 +1205,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // the recurrence needs a proper turn per step (0 < dt < pi, sin dt > 0); the three proofs
     // share these constants, and each has its own switch below
     proofs_valid = h.kind == RRT_METRIC_SCHWARZSCHILD && fin && h.dt > 0.0 && h.dt < 3.0 && h.sin_dt > 0.0 &&
-                   h.steps >= 1;
+                   h.steps >= 1 && in_proof_envelope(c);
     mp.on = (proofs_valid && !(p->flags & RRT_RENDER_NO_MISS_PROOF)) ? 1u : 0u;
   }
   {  // shadow-ray occlusion proof: the same recurrence, against the root box's face triangles
@@ -1457,6 +1591,16 @@ extern "C" int rrt_get_big_masks(const rrt_ctx* c, uint32_t* mask, double* reach
   if (mask && !c->big_mask.empty()) std::memcpy(mask, c->big_mask.data(), c->big_mask.size() * sizeof(uint32_t));
   if (reach) *reach = (RRT_BIG_REACH - 1) * c->hgrid.h_free;
   return (int)std::min<size_t>(c->big_mask.size(), 0x7fffffff);
+}
+
+extern "C" int rrt_get_search_tree(const rrt_ctx* c, double* boxes, int32_t* nodes) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  for (size_t i = 0; i < c->free_tree.size(); ++i) {
+    const DNode& n = c->free_tree[i];
+    if (boxes) for (int k = 0; k < 3; ++k) { boxes[6 * i + k] = n.mn[k]; boxes[6 * i + 3 + k] = n.mx[k]; }
+    if (nodes) { nodes[4 * i] = n.skip; nodes[4 * i + 1] = n.first; nodes[4 * i + 2] = n.count; nodes[4 * i + 3] = n.pad; }
+  }
+  return (int)c->free_tree.size();
 }
 
 extern "C" int rrt_get_clean_tree(const rrt_ctx* c, double* boxes, int32_t* nodes, double* big_boxes,

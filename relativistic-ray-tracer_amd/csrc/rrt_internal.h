@@ -152,6 +152,7 @@ struct KParams {
   double big_reach;           // segments shorter than this may use big_mask ((RRT_BIG_REACH - 1) h_free)
   int32_t clean_root;         // 0, or -1 if every leaf is oversized
   uint32_t n_big;
+  const DNode* free_nodes;    // search tree over the clean tree's leaves (traverse_free), or null
   DCamera cam;
   DHole hole;
   DMissProof miss;

@@ -26,6 +26,7 @@ RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_P
 RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED, RRT_RENDER_NO_FIRST = 256, 512, 1024
 RRT_RENDER_ONE_QUEUE, RRT_RENDER_XCD_QUEUES, RRT_RENDER_NO_MISS_PROOF, RRT_RENDER_PREPASS = 2048, 4096, 8192, 16384
 RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF, RRT_RENDER_NO_PIXEL_PROOF = 1 << 15, 1 << 16, 1 << 17
+RRT_RENDER_NO_SEARCH_TREE = 1 << 18
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 
@@ -92,7 +93,7 @@ class Stats(C.Structure):
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)
 EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
            "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
-           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_launch_times", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree",
+           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_launch_times", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree", "rrt_get_search_tree", "rrt_proof_envelope",
            "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load",
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
@@ -136,8 +137,10 @@ def lib():
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_launch_times.argtypes = [vp, C.c_uint32, vp, vp]
+        L.rrt_proof_envelope.argtypes = [vp]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
-        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_big_masks", 3),
+        for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_search_tree", 3),
+                             ("rrt_get_big_masks", 3),
                              ("rrt_get_occluders", 3)):
             if hasattr(L, name):  # absent from older builds loaded through RRT_LIB
                 getattr(L, name).argtypes = [vp] * n_args
@@ -451,6 +454,20 @@ class Renderer:
         big = np.zeros((max(s.n_big, 1), 3), np.int32)
         self._chk(0 if lib().rrt_get_clean_tree(self.h, _p(boxes), _p(nodes), _p(bb), _p(big)) > 0 else RRT_E_INVALID)
         return boxes, nodes, bb[:s.n_big], big[:s.n_big]
+
+    def proof_envelope(self):
+        """True if the scene and hole lie in the proofs' validated envelope (rrt_proof_envelope)."""
+        return lib().rrt_proof_envelope(self.h) == 1
+
+    def search_tree(self):
+        """(boxes [n,6], nodes [n,4] (skip, first, count, ordinal)) of the search tree, or None."""
+        n = lib().rrt_get_search_tree(self.h, None, None)
+        if n <= 0:
+            return None
+        boxes = np.zeros((n, 6), np.float64)
+        nodes = np.zeros((n, 4), np.int32)
+        lib().rrt_get_search_tree(self.h, _p(boxes), _p(nodes))
+        return boxes, nodes
 
     def bvh(self):
         s = self.stats()

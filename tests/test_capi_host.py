@@ -314,3 +314,74 @@ def test_clean_walk_matches_reference_walk(host_ctx, scene):
         assert ref[:2] == got[:2], (i, ref, got)
         n_hit += ref[0] >= 0
     assert n_hit > 20
+
+
+@pytest.mark.parametrize("scene", ["CBbunny", "CBcoil", "CBgems"])
+def test_search_walk_matches_reference_walk(host_ctx, scene):
+    """traverse_free (search tree): the SAH hierarchy holds exactly the clean tree's
+    leaves (the reference's leaf boxes and slot runs) under inner boxes that contain them, and its
+    walk at the full max_t followed by the ordered replay of the accepted primitives -- in windows
+    of 4 slots, and of 1 to exercise the window edges -- returns the reference walk's closest hit
+    (leaf slot and t, bit for bit) and its any-hit answer."""
+    from walk_sim import Walker
+    path = os.path.join(GOLD, "scenes", scene + ".rrts")
+    host_ctx.set_scene(rrt.SceneFile(path))
+    ct = host_ctx.clean_tree()
+    st = host_ctx.search_tree()
+    assert st is not None
+    sb, sn = st
+    cb, cn = ct[0], ct[1]
+    leaves_clean = sorted((int(r[1]), int(r[2]), tuple(cb[i])) for i, r in enumerate(cn) if r[2] > 0)
+    leaves_search = sorted((int(r[1]), int(r[2]), tuple(sb[i])) for i, r in enumerate(sn) if r[2] > 0)
+    assert leaves_clean == leaves_search
+    # pre-order with skip pointers; every inner box contains its subtree
+    n = len(sn)
+    end = [0] * n
+    for i in range(n - 1, -1, -1):
+        end[i] = i + 1 if sn[i][2] > 0 else end[end[i + 1]]
+        assert sn[i][0] == (end[i] if end[i] < n else -1)
+        if sn[i][2] == 0:
+            sub = sb[i + 1:end[i]]
+            assert (sb[i][:3] <= sub[:, :3]).all() and (sb[i][3:] >= sub[:, 3:]).all()
+    boxes, nodes, prims = host_ctx.bvh()
+    tris, _ = _scene_prims(path)
+    t = tris[prims.astype(np.int64)]
+    geo = np.concatenate([t[:, 0], t[:, 1] - t[:, 0], t[:, 2] - t[:, 0]], 1)
+    w = Walker(boxes, nodes, geo, ct)
+    w.planes(1e-9 * max(1.0, float(np.abs(boxes[0]).max())))
+    w.set_search_tree(st)
+    rng = np.random.default_rng(5)
+    lo, hi = boxes[0, :3], boxes[0, 3:]
+    n_hit = n_multi = 0
+    for i in range(300):
+        if i % 3 == 0:    # long segments through the geometry: several accepted primitives
+            k = rng.integers(len(t))
+            tgt = rng.dirichlet([1, 1, 1]) @ t[k]
+            dv = rng.normal(size=3)
+            dv /= np.linalg.norm(dv)
+            o = tgt - dv * rng.uniform(0.2, 1.0)
+            L = rng.uniform(0.5, 2.5)
+        elif i % 3 == 1:  # near a primitive, short, often grazing
+            k = rng.integers(len(t))
+            tgt = rng.dirichlet([1, 1, 1]) @ t[k]
+            o = tgt + rng.normal(0, 0.05, 3)
+            L = rng.uniform(0.01, 0.3)
+            dv = rng.normal(size=3)
+        else:             # anywhere in and around the room
+            o = lo + rng.uniform(-0.5, 1.5, 3) * (hi - lo)
+            L = rng.uniform(0.05, 5)
+            dv = rng.normal(size=3)
+        if i % 7 == 0:
+            dv[rng.integers(3)] = 0.0
+        d = dv / np.linalg.norm(dv)
+        o, d = tuple(float(v) for v in o), tuple(float(v) for v in d)
+        ref = w.reference(o, d, float(L))
+        for window in (4, 1):
+            got = w.search(o, d, float(L), window=window)
+            assert ref[:2] == got[:2], (i, window, ref, got)
+            if window == 1:
+                n_multi += w.windows > 2  # two or more primitives accepted at the full max_t
+        anyh = w.search(o, d, float(L), any_hit=True)
+        assert (anyh[0] >= 0) == (ref[0] >= 0), (i, ref, anyh)
+        n_hit += ref[0] >= 0
+    assert n_hit > 30 and n_multi > 10, (n_hit, n_multi)

@@ -66,7 +66,7 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
             "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
-            "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF}
+            "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -83,7 +83,7 @@ def test_small_cases(gpu, name, variant):
 PROOFS = {"proofs": 0,
           "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF | rrt.RRT_RENDER_NO_PIXEL_PROOF,
           "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
-          "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF}
+          "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE}
 
 
 @pytest.mark.parametrize("proof", sorted(PROOFS))

@@ -3,6 +3,8 @@
 reference_walk: BVHAccel::intersect_micro (bvh.cpp:115-138) over the reference tree -- left-first,
 every accepted primitive shrinks max_t (t <= max_t: a later equal t wins).
 clean_walk: rrt_device.h traverse_clean over the clean tree plus the oversized-leaf list.
+search: rrt_device.h traverse_free -- the SAH search tree's walk at the full max_t, then the ordered
+replay of the accepted primitives in windows of `window` slots.
 Both use IEEE double arithmetic with the reference's operation order (Python floats), and
 std::min/max semantics, so their answers can be compared exactly."""
 import numpy as np
@@ -69,6 +71,79 @@ class Walker:
             self.cboxes = [tuple(b) for b in cb]
             self.cnodes = [tuple(int(v) for v in r) for r in cn]
             self.big = [(tuple(bb[i]), int(bg[i, 0]), int(bg[i, 1]), int(bg[i, 2])) for i in range(len(bg))]
+
+    def set_search_tree(self, st):
+        """st: rrt.Renderer.search_tree() -> (boxes, nodes (skip, first, count, ordinal))."""
+        boxes, nodes = st
+        self.sboxes = [tuple(b) for b in boxes]
+        self.snodes = [tuple(int(v) for v in r) for r in nodes]
+
+    def _tri_or_sphere(self, s, o, d, max_t):
+        g = self.geo[s]
+        return tri(g[0:3], g[3:6], g[6:9], o, d, max_t)
+
+    def search(self, o, d, max_t, window=4, any_hit=False):
+        """traverse_free: (slot, t) of the closest hit (or (-1, max_t)), and the box tests."""
+        tests = 1
+        if not slab(self.boxes[0], o, d, max_t):
+            return -1, max_t, tests
+        L = max_t
+        e = tuple(o[k] + d[k] * L for k in range(3))
+        m, hit, after, cut, cut_pass = L, -1, -1, None, False
+        self.windows = 0
+        while True:
+            self.windows += 1
+            acc = []  # (slot, leaf ref) accepted at L with slot > after
+
+            def take(first, count, ref):
+                for s in range(first, first + count):
+                    if s <= after or not self._may(s, o, e):
+                        continue
+                    if self._tri_or_sphere(s, o, d, L) is not None:
+                        acc.append((s, ref))
+
+            for bi, (box, first, count, _) in enumerate(self.big):
+                if any(self._may(s, o, e) for s in range(first, first + count)):
+                    tests += 1
+                    if slab(box, o, d, L):
+                        take(first, count, ("big", bi))
+            node = 0
+            while node >= 0:
+                tests += 1
+                skip, first, count, _ = self.snodes[node]
+                if not slab(self.sboxes[node], o, d, L):
+                    node = skip
+                    continue
+                if count == 0:
+                    node += 1
+                    continue
+                take(first, count, ("tree", node))
+                node = skip
+            if any_hit:
+                return (acc[0][0] if acc else -1), L, tests
+            if not acc:
+                break
+            acc.sort()
+            more = len(acc) > window
+            acc = acc[:window]
+            cur, passed = None, False
+            for s, ref in acc:
+                if ref != cur:
+                    cur = ref
+                    if ref == cut and after >= 0:
+                        passed = cut_pass
+                    else:
+                        box = self.big[ref[1]][0] if ref[0] == "big" else self.sboxes[ref[1]]
+                        passed = slab(box, o, d, m)
+                if not passed:
+                    continue
+                r = self._tri_or_sphere(s, o, d, m)
+                if r is not None:
+                    m, hit = r[0], s
+            if not more:
+                break
+            after, cut, cut_pass = acc[-1][0], acc[-1][1], passed
+        return hit, m, tests
 
     def planes(self, eps):
         """Supporting planes for the cull of rrt_device.h plane_may_hit (rrt_host.cpp)."""

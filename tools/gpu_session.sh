@@ -54,7 +54,7 @@ for step in "$@"; do
     ab)    run ab 900 python3 tools/ab_kernels.py --rounds ${AB_ROUNDS:-3} ${AB_VARIANTS:-lean1:0:1 lean2:0:2 lean3:0:3 lean4:0:4 mega2:4:2} ;;
     avail) run avail 120 rocprofv3 --list-avail ;;
     ubench) run ubench_f64 300 ./tools/ubench_f64 ;;
-    crop)  # the cfg3 lit streak alone on an idle GPU: the per-pixel latency floor of the frame's tail
+    cropfloor)  # the cfg3 lit streak alone on an idle GPU: the per-pixel latency floor of the frame's tail
            run crop_streak 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0 &&
            run crop_tiles 300 python3 tools/crop_probe.py --region 960 576 32 64 --no-counters --flags 0 ;;
     valu)  # PMC passes over the bench's launches (-> tools/pmc_valu.py): FP64 VALU mix, lane utilisation,
@@ -67,6 +67,13 @@ for step in "$@"; do
     cropw) # the streak crop at 2..5 waves/SIMD (register budget vs spills) and its phase profile
            run cropw 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0:2 0:3 0:4 0:5 &&
            RRT_LIB=tools/_var/librrt_prof.so run crop_phase 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
+    cropd) # the streak crop without walks (diagnostic flags; results are not the reference's) and its counters
+           run cropd 300 python3 tools/crop_probe.py --region 960 600 24 16 --flags 0 1073741824 268435456 536870912 65536 ;;
+    crop)  run crop 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0 262144 ;;
+    parity) run pytest_parity 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_kerr.py tests/test_gpu_cli.py -x -q --timeout 300 --timeout-method thread ;;
+    abtree) run abtree3 600 python3 tools/ab_workload.py --workload cfg3 --rounds 3 0 0:262144 &&
+            run abtree4 600 python3 tools/ab_workload.py --workload cfg4 --rounds 2 0 0:262144 &&
+            run abtree5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 0:262144 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
