@@ -49,6 +49,9 @@ WORKLOADS = {
     "cfg4": dict(dae="@cfg4", w=3840, h=2160, spp=256, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=32,
                  desc="cfg4: torus knot (100k tris, CBdragon substitute) in CBempty, 3840x2160 256spp, "
                       "Schwarzschild, depth 1"),
+    "m3": dict(dae="CBspheres_lambertian.dae", w=1920, h=1080, spp=64, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=24,
+               depth=3, desc="m3: CBspheres_lambertian.dae 1920x1080 64spp, Schwarzschild, max_ray_depth 3 "
+                             "(at_least_one_bounce_radiance, part1_code.cpp:69-101)"),
     "cfg5": dict(dae="CBbunny.dae", w=3840, h=2160, spp=1024, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=24,
                  kerr=(0.9, (0.0, 1.0, 0.0)), env="@sky",
                  desc="cfg5: CBbunny.dae 3840x2160 1024spp, Kerr a/M 0.9 (axis +y, r_s 0.1, dtheta 0.1) + "
@@ -182,7 +185,8 @@ def cpu_baseline(wl, threads, row_stride, scene_path, camera_path, env=None):
         s.set_envmap(env)
     cam = O.load_camera(camera_path)
     c, r_s, dt = wl["bh"]
-    p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], bh=(c[0], c[1], c[2], r_s, dt), kerr=wl.get("kerr"))
+    p = O.make_params(wl["w"], wl["h"], ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), bh=(c[0], c[1], c[2], r_s, dt),
+                      kerr=wl.get("kerr"))
     rows = list(range(row_stride // 2, wl["h"], row_stride))
     samples = 0
     t0 = time.perf_counter()
@@ -303,7 +307,8 @@ def main():
     r.set_envmap(env)
     kerr = wl.get("kerr")
     r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
-    params = rrt.render_params(W, H, ns_aa=wl["spp"], variant=a.variant)
+    depth = wl.get("depth", 1)
+    params = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=depth, variant=a.variant)
 
     plan = rrt_frame.FramePlan(W, H, world, TILE)
     tiles = plan.tiles(rank)
@@ -368,7 +373,7 @@ def main():
     def count_pass(flags):
         ctr = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
         tmp = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
-        cparams = rrt.render_params(W, H, ns_aa=wl["spp"], flags=rrt.RRT_RENDER_COUNTERS | flags)
+        cparams = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=depth, flags=rrt.RRT_RENDER_COUNTERS | flags)
         r.render_tiles_device(cparams, tiles, TILE, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
                               d_counters=ctr.data_ptr(), stream=s_handle)
         torch.cuda.synchronize()

@@ -245,6 +245,19 @@ int rrt_unpack_tiles_device(rrt_ctx* ctx, const uint32_t* tiles, uint32_t n_tile
  * (image.h:53-62, 183-198), frame layout on the device. */
 int rrt_tonemap_device(rrt_ctx* ctx, uint32_t n_pixels, const float* d_rgb, uint32_t* d_rgba, void* stream);
 
+/* Multi-GPU group: one frame region over several contexts, one per GPU (the
+ * reference's tile worker pool, pathtracer.cpp:251-255, 279-281, 611-644, as one launch per GPU).
+ * The region's 32x32 tiles are dealt block-cyclically (serpentine), every member renders its
+ * tiles into a packed buffer on its own stream, member 0 gathers them -- RCCL grouped
+ * send / recv over xGMI when the members are on distinct devices, device copies when several
+ * share one -- and unpacks them.  Output as rrt_render (host buffers [h][w]).  The contexts must
+ * hold the same scene, camera and spacetime; the group does not own them. */
+typedef struct rrt_group rrt_group;
+int rrt_group_create(rrt_ctx* const* ctxs, uint32_t n, rrt_group** out);
+int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                     float* rgb_out, int32_t* count_out, const volatile int* cancel);
+void rrt_group_destroy(rrt_group* g);
+
 /* Block-cyclic tile partition of a frame over `world` ranks (serpentine 32x32 tile order,
  * multi-GPU split of SURVEY 8(e)).  Writes up to max_tiles (x, y) pairs for `rank` into
  * tiles_out and returns the number of tiles (or a negative error). */

@@ -9,8 +9,10 @@
 //                                                lens parameters are written into it, like :126-128)
 //   set_frame_size / start_raytracing / stop /   same names, same state machine (INIT, READY,
 //   clear / render_to_file / raytrace_cell /     RENDERING, DONE); the CPU worker pool is replaced
-//   save_image / save_sampling_rate_image        by one dispatcher thread per context that submits
-//                                                whole bands of the frame to the GPU
+//   save_image / save_sampling_rate_image        by one dispatcher thread that submits whole bands
+//                                                of the frame to the GPU -- or, given several
+//                                                devices, to all of them (rrt_group: block-cyclic
+//                                                tiles, one context per GPU, RCCL gather)
 //   sampleBuffer / sampleCountBuffer /           sample_buffer() / sample_count_buffer() /
 //   frameBuffer                                  frame_buffer() (same layouts, y = 0 at the bottom)
 //   global_black_hole (-B)                       set_black_hole
@@ -46,6 +48,11 @@ class PathTracer {
              float max_tolerance = 0.05f, const rrt_envmap_desc* envmap = nullptr,
              bool direct_hemisphere_sample = false, std::string filename = "", double lensRadius = 0.25,
              double focalDistance = 4.7, int device = 0);
+  // the same over several GPUs (one context each, rrt_group: block-cyclic tiles, RCCL gather)
+  PathTracer(const std::vector<int>& devices, size_t ns_aa = 1, size_t max_ray_depth = 4, size_t ns_area_light = 1,
+             size_t samples_per_batch = 32, float max_tolerance = 0.05f, const rrt_envmap_desc* envmap = nullptr,
+             bool direct_hemisphere_sample = false, std::string filename = "", double lensRadius = 0.25,
+             double focalDistance = 4.7);
   ~PathTracer();
   PathTracer(const PathTracer&) = delete;
   PathTracer& operator=(const PathTracer&) = delete;
@@ -90,7 +97,10 @@ class PathTracer {
   uint64_t seed_ = 0;
   size_t band_rows_ = 0;
 
-  rrt_ctx* ctx_ = nullptr;
+  void init(const std::vector<int>& devices, const rrt_envmap_desc* envmap);
+  rrt_ctx* ctx_ = nullptr;           // ctxs_[0]
+  std::vector<rrt_ctx*> ctxs_;       // one per device
+  rrt_group* group_ = nullptr;       // several devices: the multi-GPU plan
   rrt_scene_file* scene_ = nullptr;
   rrt_camera_state* camera_ = nullptr;
   std::vector<float> envmap_texels_;

@@ -34,6 +34,7 @@ static void usage(const char* binary) {
   std::printf("  -b  <FLOAT>      Lens radius     -d <FLOAT> Focal distance\n");
   std::printf("  -B  <X> <Y> <Z> <R> <DTHETA>  Black hole centre, Schwarzschild radius, step\n");
   std::printf("  --seed <INT>     Keyed RNG seed (default 0)   --device <INT> HIP device\n");
+  std::printf("  --devices <D0,D1,...>  Render on several GPUs (block-cyclic tiles, RCCL gather)\n");
   std::printf("  --kerr <A> [<AX> <AY> <AZ>]  Kerr black hole, spin a/M in [0,1) about axis (default 0 1 0)\n");
   std::printf("  -h               Print this help message\n");
 }
@@ -50,6 +51,7 @@ int main(int argc, char** argv) {
   std::string filename, cam_settings, envmap_path, scene_path;
   unsigned long long seed = 0;
   int device = 0;
+  std::vector<int> devices;  // --devices: several GPUs (rrt_group)
   bool to_file = false;
   auto need = [&](int i, int n) {
     if (i + n >= argc) { usage(argv[0]); std::exit(1); }
@@ -83,6 +85,16 @@ int main(int argc, char** argv) {
     }
     else if (a == "--seed") { need(i, 1); seed = std::strtoull(argv[++i], nullptr, 0); }
     else if (a == "--device") { need(i, 1); device = std::atoi(argv[++i]); }
+    else if (a == "--devices") {
+      need(i, 1);
+      const std::string list = argv[++i];
+      for (size_t at = 0; at <= list.size();) {
+        const size_t comma = std::min(list.find(',', at), list.size());
+        devices.push_back(std::atoi(list.substr(at, comma - at).c_str()));
+        at = comma + 1;
+      }
+      device = devices[0];
+    }
     else if (a == "--kerr") {
       need(i, 1);
       kerr_spin = std::atof(argv[++i]);
@@ -137,8 +149,10 @@ int main(int argc, char** argv) {
     env.width = ew; env.height = eh; env.texels = env_texels.data();
     envp = &env;
   }
-  rrt::PathTracer pt(ns_aa, max_ray_depth, ns_area_light, 1, 1, 1, num_threads, samples_per_batch, max_tolerance,
-                     envp, hemi, stem, lens_radius, focal_distance, device);
+  if (devices.empty()) devices.push_back(device);
+  rrt::PathTracer pt(devices, ns_aa, max_ray_depth, ns_area_light, samples_per_batch, max_tolerance, envp, hemi, stem,
+                     lens_radius, focal_distance);
+  (void)num_threads;  // -t: the CPU worker count; the GPU's waves take its place
   pt.set_seed(seed);
   pt.set_black_hole(hole, hole[3], hole[4]);
   if (kerr_spin >= 0) pt.set_kerr(kerr_spin, kerr_axis);
@@ -151,7 +165,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "[rrt_render] %s\n", pt.last_error().empty() ? "renderer not ready" : pt.last_error().c_str());
     return 3;
   }
-  std::printf("[PathTracer] Rendering %zux%zu, %zu spp on device %d... ", fw, fh, ns_aa, device);
+  std::printf("[PathTracer] Rendering %zux%zu, %zu spp on %zu device(s) (first %d)... ", fw, fh, ns_aa,
+              devices.size(), devices[0]);
   std::fflush(stdout);
   pt.render_to_file(filename, x, y, dx, dy);
   if (pt.state() != rrt::PathTracer::DONE) {

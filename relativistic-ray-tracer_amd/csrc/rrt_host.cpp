@@ -1714,3 +1714,210 @@ extern "C" int rrt_camera_file_load(const char* path, rrt_camera_desc* out) {
   out->focalDistance = d[28]; out->lensRadius = d[29];
   return RRT_OK;
 }
+
+// ------------------------------------------------------------------------------ device groups
+// One frame region over several contexts (one per GPU): the reference's worker pool over tiles
+// (pathtracer.cpp:251-255, 279-281, 611-644) as one launch per GPU.  The region's 32x32 tiles
+// are dealt block-cyclically in serpentine order (rrt_partition_tiles' rule), every member renders
+// its tiles into one packed buffer on its own stream, and the buffers are gathered to member 0
+// -- over RCCL (grouped ncclSend / ncclRecv, xGMI between MI355X) when the members sit on
+// distinct devices, by device copies when several members share one device (a one-GPU run of
+// the same plan) -- and unpacked there into the region.  Pixels are independent under the keyed
+// RNG, so the result equals a one-context render bit for bit.  RCCL is loaded on first use
+// (dlopen, local symbols), so librrt needs no RCCL unless a group spans several devices.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+struct rrt_group {
+  std::vector<rrt_ctx*> ctx;  // not owned
+  bool distinct = false;      // every member on its own device: RCCL
+  void* rccl = nullptr;
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGetErrorString) err_str = nullptr;
+  std::vector<ncclComm_t> comm;
+  std::vector<int32_t*> packed;  // per member, on its device: [n_max * T^2 * 3] f32 rgb, [n_max * T^2] i32 count
+  std::vector<int32_t*> inbox;   // on member 0's device, one per other member
+  size_t words = 0;              // capacity of each packed / inbox buffer, int32 words
+  float* frame_rgb = nullptr;    // the whole frame on member 0 (unpack target)
+  int32_t* frame_cnt = nullptr;
+  size_t frame_px = 0;
+  std::vector<hipEvent_t> ready;  // per member: its packed buffer is written (device-copy gather)
+};
+
+static int group_fail(rrt_group* g, int code, const std::string& msg) { return fail(g->ctx[0], code, msg); }
+#define GCHK(g, x)                                                                                    \
+  do {                                                                                                \
+    hipError_t e_ = (x);                                                                              \
+    if (e_ != hipSuccess) return group_fail(g, RRT_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCHK(g, x)                                                                                   \
+  do {                                                                                               \
+    ncclResult_t r_ = (x);                                                                           \
+    if (r_ != ncclSuccess) return group_fail(g, RRT_E_HIP, std::string(#x) + ": " + g->err_str(r_)); \
+  } while (0)
+
+static int group_load_rccl(rrt_group* g) {
+  g->rccl = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!g->rccl) g->rccl = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+  if (!g->rccl) return group_fail(g, RRT_E_HIP, std::string("cannot load RCCL: ") + dlerror());
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(g->rccl, name));
+    return fn != nullptr;
+  };
+  if (!(sym(g->comm_init_all, "ncclCommInitAll") && sym(g->comm_destroy, "ncclCommDestroy") &&
+        sym(g->group_start, "ncclGroupStart") && sym(g->group_end, "ncclGroupEnd") && sym(g->send, "ncclSend") &&
+        sym(g->recv, "ncclRecv") && sym(g->err_str, "ncclGetErrorString")))
+    return group_fail(g, RRT_E_HIP, "RCCL lacks ncclSend / ncclRecv / ncclCommInitAll");
+  std::vector<int> devs;
+  for (rrt_ctx* c : g->ctx) devs.push_back(c->device);
+  g->comm.assign(g->ctx.size(), nullptr);
+  NCHK(g, g->comm_init_all(g->comm.data(), (int)devs.size(), devs.data()));
+  return RRT_OK;
+}
+
+extern "C" void rrt_group_destroy(rrt_group* g) {
+  if (!g) return;
+  for (size_t i = 0; i < g->ctx.size(); ++i) {
+    hipSetDevice(g->ctx[i]->device);
+    if (i < g->packed.size()) hipFree(g->packed[i]);
+    if (i < g->ready.size() && g->ready[i]) hipEventDestroy(g->ready[i]);
+  }
+  if (!g->ctx.empty()) {
+    hipSetDevice(g->ctx[0]->device);
+    for (int32_t* b : g->inbox) hipFree(b);
+    hipFree(g->frame_rgb);
+    hipFree(g->frame_cnt);
+  }
+  for (ncclComm_t cm : g->comm)
+    if (cm && g->comm_destroy) g->comm_destroy(cm);
+  if (g->rccl) dlclose(g->rccl);
+  delete g;
+}
+
+extern "C" int rrt_group_create(rrt_ctx* const* ctxs, uint32_t n, rrt_group** out) {
+  if (!out || !ctxs || n == 0) return RRT_E_INVALID;
+  *out = nullptr;
+  std::unique_ptr<rrt_group, void (*)(rrt_group*)> g(new rrt_group(), rrt_group_destroy);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!ctxs[i]) return RRT_E_INVALID;
+    if (ctxs[i]->device < 0) return fail(ctxs[i], RRT_E_NO_DEVICE, "host-only context cannot join a device group");
+    g->ctx.push_back(ctxs[i]);
+  }
+  std::vector<int> devs;
+  for (rrt_ctx* c : g->ctx) devs.push_back(c->device);
+  std::sort(devs.begin(), devs.end());
+  g->distinct = n > 1 && std::adjacent_find(devs.begin(), devs.end()) == devs.end();
+  g->ready.assign(n, nullptr);
+  for (uint32_t i = 0; i < n; ++i) {
+    GCHK(g.get(), hipSetDevice(g->ctx[i]->device));
+    GCHK(g.get(), hipEventCreateWithFlags(&g->ready[i], hipEventDisableTiming));
+  }
+  if (g->distinct)
+    if (int rc = group_load_rccl(g.get())) return rc;
+  *out = g.release();
+  return RRT_OK;
+}
+
+extern "C" int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32_t x0, uint32_t y0, uint32_t w,
+                                uint32_t h, float* rgb_out, int32_t* count_out, const volatile int* cancel) {
+  if (!g || !p || !rgb_out || !count_out) return RRT_E_INVALID;
+  if (w == 0 || h == 0) return RRT_OK;
+  if ((uint64_t)x0 + w > p->frame_w || (uint64_t)y0 + h > p->frame_h)
+    return group_fail(g, RRT_E_INVALID, "region outside frame");
+  const uint32_t n = (uint32_t)g->ctx.size(), ts = 32, T2 = ts * ts;
+  // the region's tiles, dealt block-cyclically in serpentine order
+  const uint32_t tw = (w + ts - 1) / ts, th = (h + ts - 1) / ts;
+  std::vector<std::vector<uint32_t>> tiles(n);
+  for (uint32_t ty = 0, k = 0; ty < th; ++ty)
+    for (uint32_t i = 0; i < tw; ++i, ++k) {
+      const uint32_t tx = (ty & 1) ? (tw - 1 - i) : i;
+      tiles[k % n].push_back(x0 + tx * ts);
+      tiles[k % n].push_back(y0 + ty * ts);
+    }
+  size_t n_max = 0;
+  for (const auto& t : tiles) n_max = std::max(n_max, t.size() / 2);
+  const size_t words = n_max * T2 * 4;
+  if (words > g->words) {  // (re)allocate the packed buffers and member 0's inbox
+    for (uint32_t i = 0; i < n; ++i) {
+      GCHK(g, hipSetDevice(g->ctx[i]->device));
+      if (i < g->packed.size()) hipFree(g->packed[i]);
+    }
+    g->packed.assign(n, nullptr);
+    for (uint32_t i = 0; i < n; ++i) {
+      GCHK(g, hipSetDevice(g->ctx[i]->device));
+      GCHK(g, hipMalloc(&g->packed[i], words * 4));
+    }
+    GCHK(g, hipSetDevice(g->ctx[0]->device));
+    for (int32_t* b : g->inbox) hipFree(b);
+    g->inbox.assign(n, nullptr);
+    for (uint32_t i = 1; i < n; ++i) GCHK(g, hipMalloc(&g->inbox[i], words * 4));
+    g->words = words;
+  }
+  const size_t fpx = (size_t)p->frame_w * p->frame_h;
+  if (fpx > g->frame_px) {
+    GCHK(g, hipSetDevice(g->ctx[0]->device));
+    hipFree(g->frame_rgb); hipFree(g->frame_cnt);
+    g->frame_rgb = nullptr; g->frame_cnt = nullptr;
+    GCHK(g, hipMalloc(&g->frame_rgb, fpx * 3 * sizeof(float)));
+    GCHK(g, hipMalloc(&g->frame_cnt, fpx * sizeof(int32_t)));
+    g->frame_px = fpx;
+  }
+  const size_t cnt_off = g->words / 4 * 3;  // first count word of a packed buffer
+  // every member renders its tiles (launches are asynchronous: the GPUs run together)
+  for (uint32_t i = 0; i < n; ++i) {
+    if (cancel && *cancel) return group_fail(g, RRT_E_CANCELLED, "cancelled");
+    rrt_ctx* c = g->ctx[i];
+    const uint32_t nt = (uint32_t)(tiles[i].size() / 2);
+    if (nt == 0) continue;
+    int32_t* buf = g->packed[i];
+    if (int rc = launch(c, p, tiles[i].data(), nt, ts, x0, y0, x0 + w, y0 + h, (float*)buf, buf + cnt_off, nullptr,
+                        nullptr, c->stream))
+      return rc;
+    GCHK(g, hipEventRecord(g->ready[i], c->stream));
+  }
+  // gather to member 0: the frame's only exchange
+  rrt_ctx* c0 = g->ctx[0];
+  if (g->distinct) {
+    NCHK(g, g->group_start());
+    for (uint32_t i = 1; i < n; ++i) {
+      if (tiles[i].empty()) continue;
+      NCHK(g, g->send(g->packed[i], g->words, ncclInt32, 0, g->comm[i], g->ctx[i]->stream));
+      NCHK(g, g->recv(g->inbox[i], g->words, ncclInt32, (int)i, g->comm[0], c0->stream));
+    }
+    NCHK(g, g->group_end());
+  } else {
+    GCHK(g, hipSetDevice(c0->device));
+    for (uint32_t i = 1; i < n; ++i) {
+      if (tiles[i].empty()) continue;
+      GCHK(g, hipStreamWaitEvent(c0->stream, g->ready[i], 0));
+      GCHK(g, hipMemcpyPeerAsync(g->inbox[i], c0->device, g->packed[i], g->ctx[i]->device, g->words * 4, c0->stream));
+    }
+  }
+  // unpack every member's tiles into the frame on member 0, then copy the region out
+  GCHK(g, hipSetDevice(c0->device));
+  for (uint32_t i = 0; i < n; ++i) {
+    if (tiles[i].empty()) continue;
+    const int32_t* buf = i == 0 ? g->packed[0] : g->inbox[i];
+    if (int rc = rrt_unpack_tiles_device(c0, tiles[i].data(), (uint32_t)(tiles[i].size() / 2), ts, p->frame_w,
+                                         p->frame_h, (const float*)buf, buf + cnt_off, g->frame_rgb, g->frame_cnt,
+                                         c0->stream))
+      return rc;
+  }
+  GCHK(g, hipMemcpy2DAsync(rgb_out, (size_t)w * 3 * sizeof(float), g->frame_rgb + ((size_t)y0 * p->frame_w + x0) * 3,
+                           (size_t)p->frame_w * 3 * sizeof(float), (size_t)w * 3 * sizeof(float), h,
+                           hipMemcpyDeviceToHost, c0->stream));
+  GCHK(g, hipMemcpy2DAsync(count_out, (size_t)w * sizeof(int32_t), g->frame_cnt + (size_t)y0 * p->frame_w + x0,
+                           (size_t)p->frame_w * sizeof(int32_t), (size_t)w * sizeof(int32_t), h,
+                           hipMemcpyDeviceToHost, c0->stream));
+  GCHK(g, hipStreamSynchronize(c0->stream));
+  for (uint32_t i = 1; i < n; ++i) {  // the members' streams are done too (their buffers are reused next)
+    GCHK(g, hipSetDevice(g->ctx[i]->device));
+    GCHK(g, hipStreamSynchronize(g->ctx[i]->stream));
+  }
+  return RRT_OK;
+}

@@ -105,13 +105,37 @@ PathTracer::PathTracer(size_t ns_aa, size_t max_ray_depth, size_t ns_area_light,
       samples_per_batch_(samples_per_batch), max_tolerance_(max_tolerance),
       direct_hemisphere_(direct_hemisphere_sample), filename_(std::move(filename)), lens_radius_(lensRadius),
       focal_distance_(focalDistance) {
-  rrt_device_cfg cfg;
-  std::memset(&cfg, 0, sizeof(cfg));
-  cfg.device = device;
-  int rc = rrt_create(&ctx_, &cfg);
-  if (rc != RRT_OK) {
-    err_ = "rrt_create failed (" + std::to_string(rc) + ")";
-    ctx_ = nullptr;
+  init({device}, envmap);
+}
+
+PathTracer::PathTracer(const std::vector<int>& devices, size_t ns_aa, size_t max_ray_depth, size_t ns_area_light,
+                       size_t samples_per_batch, float max_tolerance, const rrt_envmap_desc* envmap,
+                       bool direct_hemisphere_sample, std::string filename, double lensRadius, double focalDistance)
+    : ns_aa_(ns_aa), max_ray_depth_(max_ray_depth), ns_area_light_(ns_area_light),
+      samples_per_batch_(samples_per_batch), max_tolerance_(max_tolerance),
+      direct_hemisphere_(direct_hemisphere_sample), filename_(std::move(filename)), lens_radius_(lensRadius),
+      focal_distance_(focalDistance) {
+  init(devices.empty() ? std::vector<int>{0} : devices, envmap);
+}
+
+// one context per device (every setter is applied to all of them); several: a device group
+void PathTracer::init(const std::vector<int>& devices, const rrt_envmap_desc* envmap) {
+  for (int device : devices) {
+    rrt_device_cfg cfg;
+    std::memset(&cfg, 0, sizeof(cfg));
+    cfg.device = device;
+    rrt_ctx* c = nullptr;
+    const int rc = rrt_create(&c, &cfg);
+    if (rc != RRT_OK) {
+      err_ = "rrt_create failed on device " + std::to_string(device) + " (" + std::to_string(rc) + ")";
+      return;
+    }
+    ctxs_.push_back(c);
+  }
+  ctx_ = ctxs_[0];
+  if (ctxs_.size() > 1 && rrt_group_create(ctxs_.data(), (uint32_t)ctxs_.size(), &group_) != RRT_OK) {
+    err_ = std::string("rrt_group_create failed: ") + rrt_last_error(ctx_);
+    group_ = nullptr;
     return;
   }
   if (envmap && envmap->texels) {  // the reference keeps the pointer; this copy owns the texels
@@ -119,7 +143,8 @@ PathTracer::PathTracer(size_t ns_aa, size_t max_ray_depth, size_t ns_area_light,
     envmap_ = *envmap;
     envmap_.texels = envmap_texels_.data();
     has_envmap_ = true;
-    if (rrt_set_envmap(ctx_, &envmap_) != RRT_OK) err_ = rrt_last_error(ctx_);
+    for (rrt_ctx* c : ctxs_)
+      if (rrt_set_envmap(c, &envmap_) != RRT_OK) err_ = rrt_last_error(c);
   }
   apply_spacetime();
 }
@@ -132,24 +157,28 @@ void PathTracer::apply_spacetime() {
   st.r_s = hole_rs_; st.delta_theta = hole_dt_;
   st.spin = kerr_spin_ < 0 ? 0.0 : kerr_spin_;
   for (int i = 0; i < 3; ++i) st.axis[i] = kerr_axis_[i];
-  if (ctx_ && rrt_set_spacetime(ctx_, &st) != RRT_OK) err_ = rrt_last_error(ctx_);
+  for (rrt_ctx* c : ctxs_)
+    if (rrt_set_spacetime(c, &st) != RRT_OK) err_ = rrt_last_error(c);
 }
 
 PathTracer::~PathTracer() {
   stop();
   if (thread_.joinable()) thread_.join();
   if (scene_) rrt_scene_file_free(scene_);
-  if (ctx_) rrt_destroy(ctx_);
+  if (group_) rrt_group_destroy(group_);
+  for (rrt_ctx* c : ctxs_) rrt_destroy(c);
 }
 
 void PathTracer::set_scene(rrt_scene_file* scene) {
   if (state_ != INIT) return;
   if (scene_ && scene_ != scene) rrt_scene_file_free(scene_);
   scene_ = scene;
-  if (!ctx_ || rrt_set_scene(ctx_, rrt_scene_file_desc(scene_)) != RRT_OK) {
-    err_ = ctx_ ? rrt_last_error(ctx_) : "no context";
-    return;
-  }
+  if (!ctx_) { err_ = "no context"; return; }
+  for (rrt_ctx* c : ctxs_)
+    if (rrt_set_scene(c, rrt_scene_file_desc(scene_)) != RRT_OK) {
+      err_ = rrt_last_error(c);
+      return;
+    }
   if (has_valid_configuration()) state_ = READY;
 }
 
@@ -160,10 +189,12 @@ void PathTracer::set_camera(rrt_camera_state* camera) {
   camera_->focalDistance = focal_distance_;
   rrt_camera_desc d;
   rrt_camera_state_desc(camera_, &d);
-  if (!ctx_ || rrt_set_camera(ctx_, &d) != RRT_OK) {
-    err_ = ctx_ ? rrt_last_error(ctx_) : "no context";
-    return;
-  }
+  if (!ctx_) { err_ = "no context"; return; }
+  for (rrt_ctx* c : ctxs_)
+    if (rrt_set_camera(c, &d) != RRT_OK) {
+      err_ = rrt_last_error(c);
+      return;
+    }
   if (has_valid_configuration()) state_ = READY;
 }
 
@@ -216,8 +247,8 @@ void PathTracer::start_raytracing() {
 }
 
 // One dispatcher thread (in place of the reference's worker pool, pathtracer.cpp:611-644):
-// the region goes to the GPU in bands of band_rows_ rows (all of it at once by default); the
-// cancel flag is polled between bands (and by rrt_render before each launch).
+// the region goes to the GPU -- or to every GPU of the group -- in bands of band_rows_ rows (all
+// of it at once by default); the cancel flag is polled between bands (and before each launch).
 void PathTracer::worker() {
   const auto t0 = std::chrono::steady_clock::now();
   const size_t x0 = cell_x0_, y0 = cell_y0_, x1 = cell_x1_, y1 = cell_y1_;
@@ -232,8 +263,10 @@ void PathTracer::worker() {
     const size_t h = std::min(band, y1 - y);
     rgb.assign(w * h * 3, 0.f);
     cnt.assign(w * h, 0);
-    const int rc = rrt_render(ctx_, &p, (uint32_t)x0, (uint32_t)y, (uint32_t)w, (uint32_t)h, rgb.data(), cnt.data(),
-                              nullptr, nullptr, &cancel_);
+    const int rc = group_ ? rrt_group_render(group_, &p, (uint32_t)x0, (uint32_t)y, (uint32_t)w, (uint32_t)h,
+                                             rgb.data(), cnt.data(), &cancel_)
+                          : rrt_render(ctx_, &p, (uint32_t)x0, (uint32_t)y, (uint32_t)w, (uint32_t)h, rgb.data(),
+                                       cnt.data(), nullptr, nullptr, &cancel_);
     if (rc != RRT_OK) {
       if (rc != RRT_E_CANCELLED) err_ = rrt_last_error(ctx_);
       ok = false;

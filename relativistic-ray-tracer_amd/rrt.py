@@ -99,7 +99,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
            "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
-           "rrt_get_occluders"]
+           "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy"]
 
 _lib = None
 

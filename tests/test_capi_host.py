@@ -385,3 +385,19 @@ def test_search_walk_matches_reference_walk(host_ctx, scene):
         assert (anyh[0] >= 0) == (ref[0] >= 0), (i, ref, anyh)
         n_hit += ref[0] >= 0
     assert n_hit > 30 and n_multi > 10, (n_hit, n_multi)
+
+
+def test_group_rejects_host_contexts():
+    """rrt_group_create needs device contexts (a host-only context cannot render)."""
+    import ctypes as C
+    L = rrt.lib()
+    h = C.c_void_p()
+    cfg = rrt.DeviceCfg()
+    cfg.device = -1
+    assert L.rrt_create(C.byref(h), C.byref(cfg)) == 0
+    arr = (C.c_void_p * 2)(h.value, h.value)
+    g = C.c_void_p()
+    L.rrt_group_create.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    assert L.rrt_group_create(arr, 2, C.byref(g)) == rrt.RRT_E_NO_DEVICE
+    assert L.rrt_group_create(None, 0, C.byref(g)) == rrt.RRT_E_INVALID
+    L.rrt_destroy(h)

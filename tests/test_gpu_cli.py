@@ -29,6 +29,23 @@ def test_cli_png_matches_reference(case, tmp_path):
     assert np.array_equal(read_png(str(tmp_path / "out_rate.png")), read_png(os.path.join(GOLD, case, "ref_rate.png")))
 
 
+@pytest.mark.parametrize("case", ["cfg1_spheres_480x360_s8", "bunny_1080p_s64_crop"])
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_cli_device_group_matches_reference(case, devices, tmp_path):
+    """--devices: rrt::PathTracer over a device group (rrt_group: one context per listed GPU,
+    block-cyclic tiles, gather to member 0 and unpack).  On one GPU the members share the device,
+    so the gather takes device copies (RCCL needs distinct devices); the partition, the packed
+    buffers and the unpack are the multi-GPU plan's, and the PNGs must still equal the reference's."""
+    info = json.load(open(os.path.join(GOLD, case, "case.json")))
+    out = str(tmp_path / "out.png")
+    cmd = [CLI] + info["args"] + ["--devices", devices, "-f", out, os.path.join(GOLD, "dae", info["dae"])]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    print(r.stdout[-400:], r.stderr[-400:])
+    assert r.returncode == 0 and "device(s)" in r.stdout
+    assert np.array_equal(read_png(out), read_png(os.path.join(GOLD, case, "ref.png")))
+    assert np.array_equal(read_png(str(tmp_path / "out_rate.png")), read_png(os.path.join(GOLD, case, "ref_rate.png")))
+
+
 def test_cli_usage_and_errors(tmp_path):
     assert subprocess.run([CLI], capture_output=True).returncode == 1
     r = subprocess.run([CLI, "-f", str(tmp_path / "x.png"), "/nonexistent.dae"], capture_output=True, text=True)

@@ -24,6 +24,10 @@ for step in "$@"; do
     bench) run bench 600 python3 bench.py --steps 5 --warmup 2 ;;
     bench4) run bench4 600 python3 bench.py --workload cfg4 --steps 2 --warmup 1 ;;
     bench5) run bench5 900 python3 bench.py --workload cfg5 --steps 1 --warmup 1 ;;
+    bench2) run bench2 600 python3 bench.py --workload cfg2 --steps 5 --warmup 2 ;;
+    benchm3) run benchm3 900 python3 bench.py --workload m3 --steps 2 --warmup 1 ;;
+    prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2 -o run --output-format csv -- python3 bench.py --workload cfg2 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    profm3) run profm3 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profm3 -o run --output-format csv -- python3 bench.py --workload m3 --steps 2 --warmup 1 --no-cpu-baseline ;;
     traffic) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 def:0:0
            run traffic 60 python3 tools/pmc_traffic.py ;;
@@ -48,6 +52,7 @@ for step in "$@"; do
            run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0} ;;
     kerr)  run pytest_kerr 600 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 300 --timeout-method thread ;;
+    cli)   run pytest_cli 600 python3 -u -m pytest tests/test_gpu_cli.py -x -q -s --timeout 300 --timeout-method thread ;;
     abw)   run abw 900 python3 tools/ab_workload.py --workload ${AB_WORKLOAD:-cfg5} --rounds ${AB_ROUNDS:-2} ${AB_WVARIANTS:-0 0:2048} ;;
     prof5) run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline ;;
     diag)  run diag 600 python3 tools/diag_clear.py --res 64 128 192 256 ;;
@@ -74,6 +79,8 @@ for step in "$@"; do
     abtree) run abtree3 600 python3 tools/ab_workload.py --workload cfg3 --rounds 3 0 0:262144 &&
             run abtree4 600 python3 tools/ab_workload.py --workload cfg4 --rounds 2 0 0:262144 &&
             run abtree5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 0:262144 ;;
+    phase) RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
+           RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
