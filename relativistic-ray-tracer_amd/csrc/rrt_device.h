@@ -1084,16 +1084,18 @@ __device__ __forceinline__ bool camera_miss_proof(const KParams& kp, v3 o, v3 d,
 }
 // Is the camera ray (o, d) a proven miss?  Schwarzschild builds only; the reference-work
 // counting passes (COUNT without count_exec) always march exactly.
-template <bool COUNT>
+// W: the calling kernel build's tag -- one copy per build, since a callee shared by builds of
+// different waves-per-SIMD budgets takes the smallest budget's registers for all of them
+template <bool COUNT, int W>
 __device__ __noinline__ bool camera_miss_proof_call(const KParams& kp, v3 o, v3 d, Counters& cn) {
   return camera_miss_proof<COUNT>(kp, o, d, cn);
 }
-// NI: out of line (the register-heavy per-pixel-loop builds keep their occupancy)
-template <bool COUNT, bool KERR, bool NI = false>
+// NI: out of line (the register-heavy per-pixel-loop builds keep their occupancy), W its build tag
+template <bool COUNT, bool KERR, bool NI = false, int W = 0>
 __device__ __forceinline__ bool camera_proven_miss(const KParams& kp, v3 o, v3 d, Counters& cn) {
   if (KERR || !kp.miss.on || (COUNT && !kp.count_exec)) return false;
   RRT_T0(tp0);
-  const bool r = NI ? camera_miss_proof_call<COUNT>(kp, o, d, cn) : camera_miss_proof<COUNT>(kp, o, d, cn);
+  const bool r = NI ? camera_miss_proof_call<COUNT, W>(kp, o, d, cn) : camera_miss_proof<COUNT>(kp, o, d, cn);
   RRT_ACC(t_proof, tp0);
   return r;
 }

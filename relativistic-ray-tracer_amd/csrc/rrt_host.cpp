@@ -1254,7 +1254,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (mega && c->hole.kind != RRT_METRIC_SCHWARZSCHILD)
     return fail(c, RRT_E_INVALID, "the wavefront A/B kernel steps the Schwarzschild metric only");
   const uint32_t wv = p->variant & 0xffu;
-  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : (pixel_loop || mega ? 2 : 3);
+  // bounce builds: 3 waves/SIMD (m3 A/B, profiles/r03_ab_deep.jsonl: 363 / 263 / 180 / 180 ms at 1 / 2 / 3 / 4)
+  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : deep ? 3 : (pixel_loop || mega ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
@@ -1369,6 +1370,46 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
     }
   }
+  // The bounce (depth >= 2) per-pixel-loop kernel behind the pixel miss proof pass: a proven
+  // pixel's samples all miss at any depth (est_radiance returns the black miss, 2 draws each), so
+  // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
+  // centre-first order
+  bool deep_list = false;
+  if (deep && pixel_loop && !count && !mega && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
+      0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
+    deep_list = true;
+    kp.draws_miss = 2;
+    kp.n_pixels = n_tiles * ts * ts;
+    std::vector<uint32_t> order(n_tiles);
+    for (uint32_t k = 0; k < n_tiles; ++k) order[k] = k;
+    if (!(p->flags & RRT_RENDER_ORDERED)) {
+      const double cx = 0.5 * p->frame_w, cy = 0.5 * p->frame_h;
+      std::vector<double> key(n_tiles);
+      for (uint32_t k = 0; k < n_tiles; ++k) {
+        const double dx = tiles[2 * k] + 0.5 * ts - cx, dy = tiles[2 * k + 1] + 0.5 * ts - cy;
+        key[k] = dx * dx + dy * dy;
+      }
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    }
+    if (c->order_cap < n_tiles) {
+      hipFree(c->d_order); c->d_order = nullptr;
+      HIPCHK(c, hipMalloc(&c->d_order, sizeof(uint32_t) * n_tiles));
+      c->order_cap = n_tiles;
+      c->h_order.clear();
+    }
+    if (order != c->h_order) {
+      c->h_order = order;
+      HIPCHK(c, hipMemcpyAsync(c->d_order, c->h_order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice, stream));
+    }
+    kp.tile_order = c->d_order;
+    if (c->list_cap < kp.n_pixels) {
+      hipFree(c->d_list); c->d_list = nullptr;
+      HIPCHK(c, hipMalloc(&c->d_list, sizeof(uint32_t) * kp.n_pixels));
+      c->list_cap = kp.n_pixels;
+    }
+    kp.claim_list = c->d_list;
+    kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
+  }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (grid == 0) grid = 1;
@@ -1401,7 +1442,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));
   } else if (pixel_loop) {
-    std::snprintf(name, sizeof(name), "rrt_render_kernel<%s, %s, %d, ...>", tf[deep], tf[count], lean == 2 ? 0 : lean);
+    std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
+                  tf[deep], tf[count], lean == 2 ? 0 : lean);
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {

@@ -70,7 +70,7 @@ __device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isec
 // at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
 // storing each level's terms, then folded back up in the reference's evaluation order.
 template <bool COUNT, int LEAN>
-__device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn) {
+__device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn) {
   spec Ld[RRT_MAX_DEPTH], smp[RRT_MAX_DEPTH], cem[RRT_MAX_DEPTH];
   float cs[RRT_MAX_DEPTH], pd[RRT_MAX_DEPTH];
   bool child[RRT_MAX_DEPTH], dl[RRT_MAX_DEPTH];
@@ -115,10 +115,10 @@ __device__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counte
   return L;
 }
 
-template <bool DEEP, bool COUNT, int LEAN>
+template <bool DEEP, bool COUNT, int LEAN, int W = 0>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
   Isect is;
-  if (camera_proven_miss<COUNT, LEAN == V_KERR, LEAN == 0>(kp, o, d, cn) ||
+  if (camera_proven_miss<COUNT, LEAN == V_KERR, LEAN == 0, W>(kp, o, d, cn) ||
       !trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
     return (!is_lean(LEAN) && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
   spec e = emission(kp.bsdfs[is.bsdf]);
@@ -128,8 +128,8 @@ __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3
 }
 
 // PathTracer::raytrace_pixel (:125-163) with ADAPTIVE == 1, THIN_LENS == 0
-template <bool DEEP, bool COUNT, int LEAN>
-__device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
+template <bool DEEP, bool COUNT, int LEAN, int W = 0>
+__device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
   spec ret = S(0, 0, 0);
   int n = 0;  // samples taken (the reference's i after its loop; counted explicitly: the
               // `++i; break;` form was miscompiled in the register-starved bounce build)
@@ -143,7 +143,7 @@ __device__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& c
     double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
     double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
-    spec s = est_radiance<DEEP, COUNT, LEAN>(kp, g, ld3(cam.pos), unit(w), cn);
+    spec s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, ld3(cam.pos), unit(w), cn);
     ret = ret + s;
     double il = illum(s);
     s1 += il;
@@ -173,18 +173,32 @@ __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* _
   const uint32_t tpix = kp.tile_size * kp.tile_size;
   for (;;) {
     uint32_t blk = 0;
-    if (lane == 0) blk = atomicAdd(kp.block_counter, 1u);
+    if (lane == 0) blk = atomicAdd(kp.block_counter, kp.claim_list ? 64u : 1u);
     blk = __shfl(blk, 0);
-    if (blk >= kp.n_blocks) break;
-    const uint32_t t = blk / (bpt * bpt), b = blk % (bpt * bpt);
-    const uint32_t lx = (b % bpt) * 8 + (lane & 7u), ly = (b / bpt) * 8 + (lane >> 3);
+    uint32_t t, lx, ly;
+    bool mine;
+    if (kp.claim_list) {  // the pixel proof pass's list: 64 listed pixels per claim, one per lane
+      const uint32_t n_list = *kp.claim_count;
+      if (blk >= n_list) break;
+      const uint32_t e = blk + lane;
+      mine = e < n_list;
+      const uint32_t ix = mine ? (kp.claim_list[e] & 0x7fffffffu) : 0u;
+      t = kp.tile_order[ix / tpix];
+      lx = (ix % tpix) % kp.tile_size; ly = (ix % tpix) / kp.tile_size;
+    } else {
+      if (blk >= kp.n_blocks) break;
+      t = blk / (bpt * bpt);
+      const uint32_t b = blk % (bpt * bpt);
+      lx = (b % bpt) * 8 + (lane & 7u); ly = (b / bpt) * 8 + (lane >> 3);
+      mine = true;
+    }
     const uint32_t x = kp.tiles[2 * t] + lx, y = kp.tiles[2 * t + 1] + ly;
-    if (lx < kp.tile_size && ly < kp.tile_size && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 &&
+    if (mine && lx < kp.tile_size && ly < kp.tile_size && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 &&
         y < kp.clip_y1) {
       Rng g; g.key = rrt_pixel_key(kp.seed, x, y); g.ctr = 0;
       Counters cn = {0, 0, 0, 0};
       int cnt;
-      spec s = raytrace_pixel<DEEP, COUNT, LEAN>(kp, x, y, cnt, g, cn);
+      spec s = raytrace_pixel<DEEP, COUNT, LEAN, 16 * DEEP + 8 * COUNT + WAVES>(kp, x, y, cnt, g, cn);
       const size_t k = (size_t)t * tpix + (size_t)ly * kp.tile_size + lx;
       kp.rgb[3 * k] = s.r; kp.rgb[3 * k + 1] = s.g; kp.rgb[3 * k + 2] = s.b;
       kp.count[k] = cnt;
@@ -245,7 +259,17 @@ hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, i
       RRT_LAUNCH(false, false, rrt::V_KERR, 2);
     }
   } else if (deep) {
-    if (count) RRT_LAUNCH(true, true, false, 1); else RRT_LAUNCH(true, false, false, 1);
+    if (count) {
+      RRT_LAUNCH(true, true, false, 1);
+    } else {
+      switch (waves) {  // register budget (A/B): the bounce build spills below 1 wave/SIMD's 256 VGPRs
+        case 2: RRT_LAUNCH(true, false, false, 2); break;
+        case 3: RRT_LAUNCH(true, false, false, 3); break;
+        case 4: RRT_LAUNCH(true, false, false, 4); break;
+        case 1: RRT_LAUNCH(true, false, false, 1); break;
+        default: RRT_LAUNCH(true, false, false, 3); break;
+      }
+    }
   } else if (count) {
     RRT_LAUNCH(false, true, false, 1);
   } else if (lean == 1) {  // LEAN 2 (point lights) runs the general build here

@@ -42,7 +42,7 @@ def main():
     for _ in range(a.rounds):
         for v in a.variants:
             var, _, fl = v.partition(":")
-            p = rrt.render_params(W, H, ns_aa=wl["spp"], variant=int(var), flags=int(fl or 0))
+            p = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), variant=int(var), flags=int(fl or 0))
             r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
             torch.cuda.synchronize()
             times[v].append(r.stats().last_kernel_ms)

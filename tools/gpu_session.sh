@@ -81,6 +81,8 @@ for step in "$@"; do
             run abtree5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 0:262144 ;;
     phase) RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
            RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
+    abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 1 1 2 3 4 1:131072 ;;
+    deeptests) run pytest_deep 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
