@@ -99,20 +99,22 @@ N_SIMD = 1024
 
 
 def find_profile(explicit, names, workload, kernel):
-    """The first profiles/ JSON (or the explicit path) recorded for this workload and kernel --
-    numbers from another kernel build are never attached to this run's line."""
+    """The first profiles/ JSON (or the explicit path) recorded for this workload, kernel and
+    librrt.so build (rrt.build_id) -- numbers from another build are never attached to this line."""
     paths = [explicit] if explicit else [os.path.join(ROOT, "profiles", n) for n in names]
+    bid = rrt.build_id()
     for path in paths:
         if path and os.path.exists(path):
             with open(path) as f:
                 d = json.load(f)
-            if d.get("workload") == workload and kernel in (d.get("kernel"), d.get("main_kernel")):
+            if (d.get("workload") == workload and kernel in (d.get("kernel"), d.get("main_kernel")) and
+                    d.get("build_id") == bid):
                 d["_path"] = os.path.relpath(path, ROOT)
                 return d
     return None
 
 
-def rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc):
+def rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc, out_bytes=0.0):
     """The dominant kernel against its real bound, FP64 VALU issue (PMC, profiles/r03_*_pmc.json),
     and against HBM on the survey's algorithmic bytes, both per launch of that
     kernel over its HIP-event time in this run.  The algorithmic bytes are reads of a scene that
@@ -123,8 +125,11 @@ def rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, 
     src = pmc if (pmc and pmc.get("hbm_bytes") is not None) else traffic
     hbm = {"bound": "hbm", "achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
            "traffic": src.get("hbm_bytes", src.get("hbm_bytes_per_launch")) if src else None,
-           "traffic_scratch": src.get("scratch_bytes") if src else None,
-           "traffic_other": src.get("other_bytes") if src else None,
+           # WRITE_SIZE beyond the kernel's outputs is register-spill scratch (the kernel writes nothing
+           # else); FETCH_SIZE mixes scratch reloads with scene reads that miss L2
+           "traffic_scratch_writes": max(src["write_bytes"] - out_bytes, 0.0) if src and "write_bytes" in src else None,
+           "traffic_fetch": src.get("fetch_bytes") if src else None,
+           "output_bytes": out_bytes,
            "traffic_source": src["_path"] if src else None,
            "kernel": main_kernel, "kernel_ms": main_ms, "launch": kernel_name,
            "algorithmic_bytes_per_launch": float(loc_bytes),
@@ -426,7 +431,8 @@ def main():
             "work_per_sample_reference": work,
             "work_per_sample_executed": xwork,
         }
-        out.update(rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc))
+        out.update(rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc,
+                             out_bytes=float(BYTES_PIXEL * pix_local)))
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or host_cores()
             out["cpu_baseline"] = cpu_baseline(wl, threads, a.cpu_row_stride or wl["row_stride"], scene_path,

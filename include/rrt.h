@@ -202,6 +202,8 @@ enum {
                                      instead of the SAH search tree over the same leaves with the
                                      ordered replay of accepted primitives (A/B; results are
                                      identical) */
+  RRT_RENDER_DEEP_SAMPLE = 1u << 19, /* depth >= 2 (Schwarzschild): the per-sample refill kernel
+                                     instead of the per-pixel loop (A/B; results are identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of

@@ -1244,10 +1244,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
   const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
-  const bool pixel_loop = deep || (p->flags & RRT_RENDER_PIXEL_LOOP);
   // kernel variant (rrt_device.h): the Kerr builds for a Kerr spacetime; else LEAN builds when
   // the scene allows (no environment map, importance-sampled direct light), else general
   const bool kerr = c->hole.kind == RRT_METRIC_KERR;
+  // bounce paths (depth >= 2): the per-pixel-loop kernel by default; RRT_RENDER_DEEP_SAMPLE selects
+  // the per-sample refill kernel (rrt_sample.hip, one lane per pixel, a lane whose pixel is done
+  // takes the next at the next sample boundary) -- m3 A/B, profiles/r03_ab_deep.jsonl: 177 ms
+  // pixel loop vs 236 ms refill at 3 waves/SIMD, identical outputs
+  const bool deep_sample = deep && !count && !kerr && (p->flags & RRT_RENDER_DEEP_SAMPLE) &&
+                           !(p->flags & RRT_RENDER_PIXEL_LOOP);
+  const bool pixel_loop = (deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP);
   const int lean = kerr ? 3 /* V_KERR */
                         : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
   if (mega && c->env_w) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel has no environment-map path");
@@ -1375,7 +1381,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
   // centre-first order
   bool deep_list = false;
-  if (deep && pixel_loop && !count && !mega && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
+  if (deep && !count && !mega && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
       0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
     deep_list = true;
     kp.draws_miss = 2;
@@ -1448,7 +1454,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {
-    std::snprintf(name, sizeof(name), "rrt_sample_kernel<%s, %d, ...>", tf[count], lean);
+    std::snprintf(name, sizeof(name), "%srrt_sample_kernel<%s, %d, %d, %s>", deep_list ? "rrt_pixel_proof_kernel + " : "",
+                  tf[count], lean, deep_sample ? (waves == 2 || waves == 4 ? waves : 3) : waves, tf[deep_sample]);
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }

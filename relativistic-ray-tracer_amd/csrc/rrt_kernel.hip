@@ -7,113 +7,9 @@
 // traversal is stackless over skip pointers (rrt_internal.h DNode), which visits exactly the
 // reference's left-then-right recursion order.  The depth <= 1 hot path runs in the
 // wavefront state-machine kernel of rrt_mega.hip instead.
-#include "rrt_device.h"
+#include "rrt_integrator.h"
 
 namespace rrt {
-
-// ------------------------------------------------------------------ integrator (part1_code.cpp)
-// `trace` = the geodesic-marched BVH query; DEEP (bounce) builds and depth <= 1 builds share it.
-template <bool ANY, bool COUNT, bool DEEP, int LEAN>
-__device__ __forceinline__ bool trace(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  return query<ANY, COUNT, LEAN == V_KERR>(kp, o, d, is, cn);
-}
-
-// LEAN: area/point lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample
-// (same values: make_coord_space is a pure function of the normal) instead of being kept live
-// across the shadow query, which keeps 12 VGPRs out of the traversal loop.
-template <bool COUNT, int LEAN, bool DEEP>
-__device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :33-57
-  const DBsdf b = kp.bsdfs[is.bsdf];
-  spec L = S(0, 0, 0);
-  int total = 0;
-  for (uint32_t li = 0; li < kp.n_lights; ++li) {
-    const DLight& l = kp.lights[li];
-    int num = l.is_delta ? 1 : (int)kp.ns_area_light;
-    total += num;
-    for (int i = 0; i < num; ++i) {
-      v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L<LEAN>(kp.env, l, g, is.hit_p, wi_world, dist, pdf);
-      const Frame f = coord_space(is.n);
-      v3 w_in = to_local(f, wi_world);
-      if (w_in.z < 0) continue;
-      spec contrib = ((sample * bsdf_f<LEAN>(b, to_local(f, is.w_out), w_in)) * (float)w_in.z) / pdf;
-      if (!trace<true, COUNT, DEEP, LEAN>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, nullptr, cn)) L = L + contrib;
-    }
-  }
-  return L / (float)total;
-}
-
-template <bool COUNT, int LEAN, bool DEEP>
-__device__ spec direct_hemisphere(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {  // :15-31
-  Frame f = coord_space(is.n);
-  v3 w_out = to_local(f, is.w_out);
-  const DBsdf b = kp.bsdfs[is.bsdf];
-  int num = (int)(kp.n_lights * kp.ns_area_light);
-  spec L = S(0, 0, 0);
-  for (int i = 0; i < num; ++i) {
-    v3 w_in = hemisphere_sample(g);
-    v3 wi_world = to_world(f, w_in);
-    Isect is2;
-    if (trace<false, COUNT, DEEP, LEAN>(kp, is.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn))
-      L = L + (emission(kp.bsdfs[is2.bsdf]) * bsdf_f(b, w_out, w_in)) * (float)w_in.z;
-  }
-  return ((L * 2.0f) * (float)PI_D) / (float)num;
-}
-
-template <bool COUNT, int LEAN, bool DEEP>
-__device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isect& is, Counters& cn) {
-  if (is_lean(LEAN)) return direct_importance<COUNT, LEAN, DEEP>(kp, g, is, cn);
-  return kp.direct_hemisphere ? direct_hemisphere<COUNT, general_of(LEAN), DEEP>(kp, g, is, cn)
-                              : direct_importance<COUNT, general_of(LEAN), DEEP>(kp, g, is, cn);
-}
-
-// at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
-// storing each level's terms, then folded back up in the reference's evaluation order.
-template <bool COUNT, int LEAN>
-__device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn) {
-  spec Ld[RRT_MAX_DEPTH], smp[RRT_MAX_DEPTH], cem[RRT_MAX_DEPTH];
-  float cs[RRT_MAX_DEPTH], pd[RRT_MAX_DEPTH];
-  bool child[RRT_MAX_DEPTH], dl[RRT_MAX_DEPTH];
-  uint32_t depth = kp.max_ray_depth;
-  int k = 0;
-  for (;; ++k) {
-    Frame f = coord_space(cur.n);
-    v3 w_out = to_local(f, cur.w_out);
-    const DBsdf b = kp.bsdfs[cur.bsdf];
-    spec L_out = S(0, 0, 0);
-    if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, general_of(LEAN), true>(kp, g, cur, cn);
-    Ld[k] = L_out;
-    child[k] = false;
-    dl[k] = is_delta(b);
-    if (depth == kp.max_ray_depth || (depth > 1 && g.coin(0.7))) {
-      v3 w_in; float pdf;
-      spec sample = bsdf_sample_f(b, g, w_out, w_in, pdf);
-      if (pdf == 0.0f) break;
-      v3 wi_world = to_world(f, w_in);
-      Isect is2;
-      if (trace<false, COUNT, true, LEAN>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
-        child[k] = true;
-        smp[k] = sample; cs[k] = (float)fabs(w_in.z); pd[k] = pdf;
-        cem[k] = emission(kp.bsdfs[is2.bsdf]);
-        cur = is2;
-        depth -= 1;
-        continue;
-      }
-    }
-    break;
-  }
-  spec L = S(0, 0, 0);
-  for (int j = k; j >= 0; --j) {
-    spec Lj = Ld[j];
-    if (child[j]) {
-      spec Lc = L;
-      if (dl[j]) Lc = Lc + cem[j];
-      Lj = Lj + (((Lc * smp[j]) * cs[j]) / pd[j]) / (float)0.7;
-    }
-    L = Lj;
-  }
-  return L;
-}
 
 template <bool DEEP, bool COUNT, int LEAN, int W = 0>
 __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123

@@ -12,7 +12,7 @@
 //   * state that is cold during a geodesic query (pixel accumulators, the shading record of the
 //     camera hit across its shadow rays) lives in LDS, one slot per lane, so the query loops run
 //     with fewer live VGPRs (more waves per SIMD hide the long FP64 dependency chains).
-#include "rrt_device.h"
+#include "rrt_integrator.h"
 
 namespace rrt {
 
@@ -146,7 +146,9 @@ extern "C" int rrt_prof_read(unsigned long long* out) {  // out: RRT_PROF_HDR + 
 
 // COUNT: per-pixel work counters; LEAN: area/point lights only, no microfacet BSDF, importance-sampled
 // direct light (the BASELINE scenes); WAVES: register budget (minimum waves per SIMD).
-template <bool COUNT, int LEAN, int WAVES>
+// DEEP: max_ray_depth >= 2 (at_least_one_bounce_radiance, part1_code.cpp:69-101) for the general
+// build; the pixels then come from the pixel miss proof pass's claim list when it ran
+template <bool COUNT, int LEAN, int WAVES, bool DEEP = false>
 __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
@@ -179,7 +181,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(kp.block_counter, 1u);
         b = __shfl(b, 0);
-        if (b >= kp.n_blocks) {
+        // a pool: one 8x8 block of a tile, or 64 entries of the pixel proof pass's claim list
+        if (b >= (kp.claim_list ? (*kp.claim_count + 63u) / 64u : kp.n_blocks)) {
           pool_empty = true;
 #if RRT_PROFILE
           if (lane == 0) atomicMin(&rrt_prof[11], (unsigned long long)wall_clock64());  // first exhaustion
@@ -196,10 +199,21 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
       const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
       if (!have && rank < avail) {
         const uint32_t k = pool_next + rank;
-        const uint32_t tl = pool_blk / (bpt * bpt), b = pool_blk % (bpt * bpt);
-        const uint32_t lx = (b % bpt) * 8 + (k & 7u), ly = (b / bpt) * 8 + (k >> 3);
+        uint32_t tl, lx, ly;
+        bool listed = true;
+        if (kp.claim_list) {
+          const uint32_t e = pool_blk * 64u + k;
+          listed = e < *kp.claim_count;
+          const uint32_t ix = listed ? (kp.claim_list[e] & 0x7fffffffu) : 0u;
+          tl = kp.tile_order[ix / tpix];
+          lx = (ix % tpix) % kp.tile_size; ly = (ix % tpix) / kp.tile_size;
+        } else {
+          tl = pool_blk / (bpt * bpt);
+          const uint32_t b = pool_blk % (bpt * bpt);
+          lx = (b % bpt) * 8 + (k & 7u); ly = (b / bpt) * 8 + (k >> 3);
+        }
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
-        if (lx < kp.tile_size && ly < kp.tile_size && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 &&
+        if (listed && lx < kp.tile_size && ly < kp.tile_size && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 &&
             y < kp.clip_y1) {
           px = x; py = y; slot = tl * tpix + ly * kp.tile_size + lx;
           g.key = rrt_pixel_key(kp.seed, x, y); g.ctr = 0;
@@ -238,6 +252,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
           query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
+        else if (DEEP && kp.max_ray_depth >= 2) s = e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
         else if (is_lean(LEAN)) s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
         else if (kp.direct_hemisphere) s = e + direct_hemisphere_lds<COUNT, LEAN>(kp, g, is, cl, t, cn);
         else s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
@@ -895,7 +910,14 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
 
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream) {
 #define RRT_LAUNCH(C, L, W) hipLaunchKernelGGL((rrt_sample_kernel<C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
-  if (count) {
+#define RRT_LAUNCH_DEEP(W) hipLaunchKernelGGL((rrt_sample_kernel<false, 0, W, true>), dim3(grid), dim3(256), 0, stream, d_kp)
+  if (!count && kp.max_ray_depth >= 2 && lean != rrt::V_KERR) {  // bounce paths, general build
+    switch (waves) {
+      case 2: RRT_LAUNCH_DEEP(2); break;
+      case 4: RRT_LAUNCH_DEEP(4); break;
+      default: RRT_LAUNCH_DEEP(3); break;
+    }
+  } else if (count) {
     if (lean == rrt::V_KERR) RRT_LAUNCH(true, rrt::V_KERR, 1); else RRT_LAUNCH(true, 0, 1);
   } else if (lean == rrt::V_KERR) {
     RRT_LAUNCH(false, rrt::V_KERR, 2);
@@ -912,5 +934,6 @@ hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, 
     RRT_LAUNCH(false, false, 2);
   }
 #undef RRT_LAUNCH
+#undef RRT_LAUNCH_DEEP
   return hipGetLastError();
 }

@@ -59,14 +59,15 @@ def check(c, rgb, cnt, draws):
 # kernel, the per-pixel-loop kernel and the wavefront state-machine kernel; the sample-parallel
 # kernel also with one chip-wide claim queue, one queue per XCD, and in list order; and the
 # default path with every camera ray marched exactly (no miss proof) and with every shadow ray
-# marched exactly (no occlusion proof)
+# marched exactly (no occlusion proof); at depth >= 2 also the per-sample refill kernel
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "xcdqueues": rrt.RRT_RENDER_XCD_QUEUES,
             "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
             "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
-            "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE}
+            "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
+            "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))

@@ -81,8 +81,20 @@ for step in "$@"; do
             run abtree5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 0:262144 ;;
     phase) RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
            RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
-    abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 1 1 2 3 4 1:131072 ;;
+    abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 2 0 2 4 0:16 0:131072 ;;
     deeptests) run pytest_deep 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
+    pmcall) # PMC of every workload's main kernel on this build, copied into profiles/ for the bench lines
+           for wk in "cfg3:rrt_batch_kernel<1, 5>" "cfg4:rrt_batch_kernel<2, 5>" "cfg5:rrt_batch_kernel<3, 3>" "cfg2:rrt_batch_kernel<1, 5>"; do
+             PMC_WORKLOAD=${wk%%:*} PMC_KERNEL=${wk#*:} bash tools/gpu_session.sh valu || exit $?
+             cp gpurun_out/r03_${wk%%:*}_pmc.json profiles/ ; done ;;
+    profall) run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+             run prof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --workload cfg4 --steps 3 --warmup 1 --no-cpu-baseline &&
+             run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline &&
+             run prof2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2 -o run --output-format csv -- python3 bench.py --workload cfg2 --steps 5 --warmup 2 --no-cpu-baseline &&
+             run profm3 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profm3 -o run --output-format csv -- python3 bench.py --workload m3 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    benchall) run bench 600 python3 bench.py --steps 5 --warmup 2 && run bench2 600 python3 bench.py --workload cfg2 --steps 5 --warmup 2 &&
+              run bench4 600 python3 bench.py --workload cfg4 --steps 2 --warmup 1 && run bench5 900 python3 bench.py --workload cfg5 --steps 1 --warmup 1 &&
+              run benchm3 900 python3 bench.py --workload m3 --steps 2 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

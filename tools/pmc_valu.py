@@ -11,6 +11,7 @@ utilisation; SQ_BUSY_CYCLES and GRBM_GUI_ACTIVE are summed over the 8 XCDs (effe
 GRBM_GUI_ACTIVE / 8 / kernel time, MI355X_MICROARCH.md 'DVFS give-back')."""
 import argparse
 import csv
+import sys
 import glob
 import json
 import os
@@ -49,7 +50,9 @@ def main():
     if not m:
         raise SystemExit(f"no dispatch of {a.kernel} in {a.dirs}")
     g = m.get
-    out = {"workload": a.workload, "main_kernel": a.kernel, "kernel": a.kernel, "counters": m,
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "relativistic-ray-tracer_amd"))
+    import rrt
+    out = {"workload": a.workload, "main_kernel": a.kernel, "kernel": a.kernel, "build_id": rrt.build_id(), "counters": m,
            "dispatches": n, "kernel_s_under_profiler": dur}
     if g("SQ_INSTS_VALU_FMA_F64") is not None:
         fma, add, mul = g("SQ_INSTS_VALU_FMA_F64", 0.0), g("SQ_INSTS_VALU_ADD_F64", 0.0), g("SQ_INSTS_VALU_MUL_F64", 0.0)
