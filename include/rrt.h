@@ -158,12 +158,14 @@ typedef struct {
   uint32_t flags;             /* RRT_RENDER_* */
   uint32_t variant;           /* A/B measurements, 0 = defaults.  Bits 0..7: waves/SIMD the
                                  depth<=1 kernel is built for (1..6, register budget); bits
-                                 8..11: the sample-0 pre-pass's waves/SIMD */
+                                 8..11: the sample-0 pre-pass's waves/SIMD; bits 16..19: the heavy-pixel
+                                 threshold (1: capture boundary only; 2 / 3 / 4: rays within
+                                 1.1 / 1.5 / 2.0 r_s; 0: 1.2) */
 } rrt_render_params;
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
   RRT_RENDER_DRAWS = 1u << 1,    /* also produce per-pixel RNG draw counts */
-  RRT_RENDER_WAVEFRONT = 1u << 2, /* depth <= 1: wavefront state-machine kernel (A/B testing) */
+  RRT_RENDER_WAVEFRONT = 1u << 2, /* removed (round 3; it lost every A/B): rejected with RRT_E_INVALID */
   RRT_RENDER_EXACT_DIV = 1u << 3, /* slab tests by true division instead of the
                                      Markstein-corrected reciprocal (A/B testing) */
   RRT_RENDER_PIXEL_LOOP = 1u << 4, /* depth <= 1: per-pixel-loop kernel instead of the default
@@ -202,6 +204,9 @@ enum {
                                      instead of the SAH search tree over the same leaves with the
                                      ordered replay of accepted primitives (A/B; results are
                                      identical) */
+  RRT_RENDER_NO_HEAVY = 1u << 20, /* sample-parallel kernel: no slot-parallel path for heavy
+                                     pixels (those whose rays straddle the hole's capture boundary
+                                     or pass close to it; A/B and parity, results are identical) */
   RRT_RENDER_DEEP_SAMPLE = 1u << 19, /* depth >= 2 (Schwarzschild): the per-sample refill kernel
                                      instead of the per-pixel loop (A/B; results are identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
@@ -278,6 +283,7 @@ typedef struct {
   char kernel[64];            /* name of the last render kernel(s) launched */
   float last_main_kernel_ms;  /* HIP-event time of the last launch's main kernel alone (after
                                  any pre-pass such as rrt_pixel_proof_kernel) */
+  uint32_t last_heavy_pixels;  /* pixels the last launch rendered slot-parallel (heavy pixels) */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 /* HIP-event times of the last n (<= 32) render launches, oldest first: the whole launch and its

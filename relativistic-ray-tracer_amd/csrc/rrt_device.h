@@ -1,5 +1,5 @@
 // rrt_device.h -- device-side restatement of the reference's math, geometry, BSDFs, lights and
-// the geodesic-marched BVH query, shared by the kernels (rrt_kernel.hip, rrt_mega.hip).
+// the geodesic-marched BVH query, shared by the kernels (rrt_kernel.hip, rrt_sample.hip).
 //
 // Numerics follow the reference exactly: double geometry (CGL Vector3D), float Spectrum with
 // the reference's narrowing points, the same operation order, no FMA contraction (the pragma
@@ -388,8 +388,9 @@ __device__ __forceinline__ int next_big_in(uint64_t m, int from, int nb) {
 //    only ones the reference can test (max_t only shrinks and the slab test is monotone in it).
 //    No primitive accepted at L  <=>  the reference finds no hit (order plays no part): done.
 //    A shadow query (ANY) stops at the first accepted primitive, as before.
-// 2. A closest-hit query keeps the slots of the primitives accepted at L (at most 4; more: the
-//    clean walk instead) with their leaves, and replays the reference on them in slot order --
+// 2. A closest-hit query keeps the slots of the primitives accepted at L (4 per window; more take
+//    further windows above the last kept slot) with their leaves, and replays the reference on
+//    them in slot order --
 //    slots are laid out in left-first leaf order, so slot order is the reference's visiting order:
 //    a leaf's box is tested once, with the max_t the reference would hold on reaching it, and its
 //    accepted primitives re-tested with that max_t.  Every other primitive the reference tests is
@@ -1222,6 +1223,63 @@ __device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px,
     rp = r; dpa = dpb; dvp = dv; ea = na; eb = nb;
   }
   return true;
+}
+
+// Heavy pixel (slot-parallel heavy pixels): some of the pixel's rays are captured
+// by the hole and some not, or its rays pass within sqrt(kp.heavy_r2) of the hole.  Such pixels
+// orbit the hole before they reach the geometry (the costliest queries of a frame) and mix hits
+// with misses (several speculation rounds per step in the batch kernel), so their slots are
+// rendered in parallel by whole batch-kernel waves (rrt_sample.hip heavy_pixel_wave).  A routing
+// heuristic only -- the pixel's result is the same on either path.  The planar recurrence
+// (camera_miss_proof) for the least and largest dx of the pixel's corners; a segment's distance
+// from the hole follows from (v_prev, v) alone.
+__device__ __forceinline__ bool pixel_heavy(const KParams& kp, uint32_t px, uint32_t py) {
+#pragma clang fp contract(fast)
+  const DMissProof& mp = kp.miss;
+  const DHole& h = kp.hole;
+  const v3 O = ld3(kp.cam.pos), c = ld3(h.c);
+  const v3 x0 = O - c;
+  const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
+  const v3 X = vmul(x0, u0);
+  double dlo = 2.0, dhi = -2.0;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const double dx = dot(pixel_ray_dir(kp, (double)px + (k & 1), (double)py + (k >> 1)), X);
+    dlo = fmin(dlo, dx);
+    dhi = fmax(dhi, dx);
+  }
+  if (!(dlo > -1.0 && dhi < 1.0)) return true;  // looking at the hole
+  const double r2 = h.r2, near2 = kp.heavy_r2, si2 = h.sin_dt * h.sin_dt, rho2 = mp.rho * mp.rho;
+  bool cap[2] = {false, false}, close = false;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double dx = i ? dhi : dlo;
+    const double up0 = -u0 * dx / sqrt(1.0 - dx * dx);
+    double vp = mp.rho * u0, s = u0 * mp.co1 - up0 * h.sin_dt * mp.inv_rho;
+#pragma unroll 1
+    for (int j = 0; j < h.steps; ++j) {
+      const double up = (vp * mp.co1 - mp.rho * s) * mp.inv_si;
+      s = fabs(vp) * mp.inv_rho;
+      const double f1 = -s + mp.k15 * s * s;
+      const double u2 = s + up * (h.dt * 0.5);
+      const double f2 = -u2 + mp.k15 * u2 * u2;
+      const double u3 = u2 + f1 * mp.dt2_4;
+      const double f3 = -u3 + mp.k15 * u3 * u3;
+      const double v = s + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
+      const double av = fabs(v), avp = fabs(vp);
+      const double D = v * v + vp * vp - 2.0 * mp.co1 * avp * v;
+      const bool inside = v * (mp.co1 * avp - v) < 0.0 && avp * (avp - mp.co1 * v) > 0.0;
+      // distance^2 from the hole below d2  <=>  inside ? si2 / D : rho^2 / max(v, vp)^2 below d2
+      const double m2 = fmax(v * v, vp * vp);
+      const bool in_r = inside ? si2 < r2 * D : rho2 < r2 * m2;
+      const bool in_n = inside ? si2 < near2 * D : rho2 < near2 * m2;
+      close = close || in_n;
+      if (in_r) { cap[i] = true; break; }
+      if (!(av > 0.0)) break;  // NaN or a degenerate step
+      vp = v;
+    }
+  }
+  return cap[0] != cap[1] || (close && !(cap[0] && cap[1]));
 }
 
 // query() behind a call: the caller keeps only what is live across the call, the walk gets the

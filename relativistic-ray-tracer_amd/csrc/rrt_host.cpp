@@ -23,7 +23,6 @@
 
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream);
-hipError_t rrt_launch_mega(const KParams& kp, const KParams* d_kp, int count, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
@@ -36,7 +35,10 @@ hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float
 namespace {
 
 constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
-constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);  // claim counters + the pixel proof's list length
+constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);  // claim counters + the pixel proof's list length + the heavy list's
+// Heavy pixels (rrt_sample.hip heavy_pixel_wave): rays passing within RRT_HEAVY_NEAR r_s of the hole (or straddling
+// its capture boundary) make a pixel heavy (profiles/r03_heavy_ab.md)
+#define RRT_HEAVY_NEAR 1.2
 
 struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
@@ -94,6 +96,9 @@ struct rrt_ctx {
   // a use on a different stream than the previous one first waits for this event
   hipEvent_t ev_fence = nullptr;
   hipStream_t fence_stream = nullptr;
+  // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
+  uint32_t* d_heavy_list = nullptr;
+  size_t heavy_list_cap = 0;
   bool fenced = false;
   int n_cu = 256;
   // host scene
@@ -160,6 +165,7 @@ struct rrt_ctx {
   float last_ms = 0.f, last_main_ms = 0.f;
   bool timed = false;
   uint32_t last_grid = 0;
+  uint32_t last_heavy = 0;  // the last launch's heavy-list capacity (0: no heavy path)
   std::string last_kernel;
 };
 
@@ -222,6 +228,7 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         !create_ring(c.get()) ||
         hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming) != hipSuccess ||
+
         hipMalloc(&c->d_counter, kCounterBytes) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
       return RRT_E_HIP;
@@ -240,6 +247,7 @@ void rrt_destroy(rrt_ctx* c) {
     free_env_dev(c);
     hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_list); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
+    hipFree(c->d_heavy_list);
     for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
       if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
       if (c->ev_main[i]) hipEventDestroy(c->ev_main[i]);
@@ -1239,11 +1247,13 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   kp.rgb = d_rgb; kp.count = d_cnt; kp.draws = d_draws; kp.counters = d_ctr;
   // Kernel choice (depth <= 1): the per-sample kernel (rrt_sample.hip) by default;
   // RRT_RENDER_PIXEL_LOOP selects the general per-pixel-loop kernel (rrt_kernel.hip, also used
-  // for depth >= 2) and RRT_RENDER_WAVEFRONT the state-machine kernel (rrt_mega.hip).  LEAN
+  // for depth >= 2).  LEAN
   // builds when the scene allows them; variant = register budget in waves per SIMD.
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
-  const bool mega = !deep && (p->flags & RRT_RENDER_WAVEFRONT);
+  // the wavefront state-machine kernel (rrt_mega.hip, an A/B variant that lost every measurement,
+  // DESIGN.md §5) was removed in round 3: its flag is rejected
+  if (p->flags & RRT_RENDER_WAVEFRONT) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel was removed");
   // kernel variant (rrt_device.h): the Kerr builds for a Kerr spacetime; else LEAN builds when
   // the scene allows (no environment map, importance-sampled direct light), else general
   const bool kerr = c->hole.kind == RRT_METRIC_KERR;
@@ -1256,19 +1266,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const bool pixel_loop = (deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP);
   const int lean = kerr ? 3 /* V_KERR */
                         : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
-  if (mega && c->env_w) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel has no environment-map path");
-  if (mega && c->hole.kind != RRT_METRIC_SCHWARZSCHILD)
-    return fail(c, RRT_E_INVALID, "the wavefront A/B kernel steps the Schwarzschild metric only");
   const uint32_t wv = p->variant & 0xffu;
   // bounce builds: 3 waves/SIMD (m3 A/B, profiles/r03_ab_deep.jsonl: 363 / 263 / 180 / 180 ms at 1 / 2 / 3 / 4)
-  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : deep ? 3 : (pixel_loop || mega ? 2 : 3);
+  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : deep ? 3 : (pixel_loop ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
   // Sample-parallel kernel (rrt_sample.hip rrt_batch_kernel) whenever a pixel takes more than
   // one sample: it needs each camera sample's RNG draw count to depend only on whether its query
   // hit, which holds at depth <= 1 (jitter + the direct-lighting samplers).
-  const bool batch = !deep && !count && !mega && !pixel_loop && std::min(p->ns_aa, p->samples_per_batch) >= 5 &&
+  const bool batch = !deep && !count && !pixel_loop && std::min(p->ns_aa, p->samples_per_batch) >= 5 &&
                      !(p->flags & RRT_RENDER_PER_PIXEL);
   if (batch) {
     kp.draws_miss = 2;
@@ -1374,6 +1381,29 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       }
       kp.claim_list = c->d_list;
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
+      // Heavy pixels (rrt_device.h pixel_heavy): the pass lists them apart and the batch kernel's
+      // first waves render them slot-parallel, a whole wave per pixel (rrt_sample.hip
+      // heavy_pixel_wave); needs a hit to take a whole number of slots (Dh = k Dm) and a step's
+      // chain to fit the wave's 64 slots
+      const uint32_t spb = std::min(p->samples_per_batch, p->ns_aa);
+      if (!(p->flags & RRT_RENDER_NO_HEAVY) && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 &&
+          (spb - 1) * (kp.draws_hit / kp.draws_miss) + 1 <= 64u) {
+        // at most 1/256 of the pixels (4096 at least): a frame mostly near the hole stays with
+        // the batch kernel, whose rounds cost less than 64 slots a step for unmixed pixels
+        const uint32_t cap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
+        if (c->heavy_list_cap < cap) {
+          hipFree(c->d_heavy_list); c->d_heavy_list = nullptr;
+          HIPCHK(c, hipMalloc(&c->d_heavy_list, sizeof(uint32_t) * cap));
+          c->heavy_list_cap = cap;
+        }
+        kp.heavy_list = c->d_heavy_list;
+        kp.heavy_count = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);
+        kp.heavy_cap = cap;
+        // A/B (variant bits 16..19): 1: capture-boundary pixels only, 2 / 3 / 4: near 1.1 / 1.5 / 2.0
+        const uint32_t nv = (p->variant >> 16) & 0xfu;
+        const double near = nv == 1 ? 0.0 : nv == 2 ? 1.1 : nv == 3 ? 1.5 : nv == 4 ? 2.0 : RRT_HEAVY_NEAR;
+        kp.heavy_r2 = (near * c->hole.r) * (near * c->hole.r);
+      }
     }
   }
   // The bounce (depth >= 2) per-pixel-loop kernel behind the pixel miss proof pass: a proven
@@ -1381,7 +1411,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
   // centre-first order
   bool deep_list = false;
-  if (deep && !count && !mega && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
+  if (deep && !count && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
       0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
     deep_list = true;
     kp.draws_miss = 2;
@@ -1443,10 +1473,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
-  } else if (mega) {
-    std::snprintf(name, sizeof(name), "rrt_mega_kernel<%s, ...>", tf[count]);
-    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
-    HIPCHK(c, rrt_launch_mega(kp, c->d_kp, count, waves, grid, stream));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   tf[deep], tf[count], lean == 2 ? 0 : lean);
@@ -1461,6 +1487,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }
   c->last_kernel = name;
+  c->last_heavy = kp.heavy_list ? kp.heavy_cap : 0u;
   HIPCHK(c, hipEventRecord(c->ev1[ring], stream));
   c->timed = true;
   ++c->n_launch;
@@ -1593,6 +1620,11 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
   }
   out->last_kernel_ms = c->last_ms;
   out->last_main_kernel_ms = c->last_main_ms;
+  if (c->device >= 0 && c->timed && c->last_heavy) {  // the pass's heavy-list length (counters persist until the next launch)
+    uint32_t n = 0;
+    if (hipMemcpy(&n, c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1), sizeof(n), hipMemcpyDeviceToHost) == hipSuccess)
+      out->last_heavy_pixels = std::min<uint32_t>(n, c->last_heavy);
+  }
   return RRT_OK;
 }
 

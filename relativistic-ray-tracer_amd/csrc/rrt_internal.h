@@ -141,7 +141,7 @@ struct KParams {
   const DBsdf* bsdfs;
   const DLight* lights;
   uint32_t n_lights;
-  uint32_t fast_div;  // scene bounds allow the Markstein-corrected slab quotients (rrt_mega.hip)
+  uint32_t fast_div;  // scene bounds allow the Markstein-corrected slab quotients
   DGrid grid;
   const DNode* clean_nodes;   // clean tree (pad = first leaf ordinal); null: reference walk only
   const DPlane* planes;       // per leaf slot; null: no plane cull
@@ -194,5 +194,12 @@ struct KParams {
   int32_t* count;
   uint32_t* draws;      // optional
   uint32_t* counters;   // optional [4] per pixel
-  DShadowProof occ;     // last: the hot fields above keep their offsets
+  DShadowProof occ;     // the hot fields above keep their offsets
+  // heavy pixels (rrt_pixel_proof_kernel pixel_heavy -> rrt_batch_kernel heavy_pixel_wave): listed
+  // pixels rendered slot-parallel, one wave per pixel and a step's 64 draw-offset slots per round
+  uint32_t* heavy_list;   // claim indices (null: no heavy path)
+  uint32_t* heavy_count;  // [0]: entries appended by the pass (capped at heavy_cap); [1]: entries taken
+  uint32_t heavy_cap;     // list capacity
+  uint32_t heavy_pad;
+  double heavy_r2;        // (RRT_HEAVY_NEAR x r_s)^2: rays passing this close make a pixel heavy
 };

@@ -6,7 +6,7 @@
 // the whole adaptive sample loop) from a device atomic over the caller's tile list.  BVH
 // traversal is stackless over skip pointers (rrt_internal.h DNode), which visits exactly the
 // reference's left-then-right recursion order.  The depth <= 1 hot path runs in the
-// wavefront state-machine kernel of rrt_mega.hip instead.
+// sample-parallel batch kernel of rrt_sample.hip instead.
 #include "rrt_integrator.h"
 
 namespace rrt {

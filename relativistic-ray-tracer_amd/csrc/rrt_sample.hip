@@ -16,13 +16,15 @@
 
 namespace rrt {
 
-// per-lane LDS slots, structure-of-arrays (consecutive lanes hit consecutive banks)
-struct ShadeLds {  // the camera hit being shaded, parked across its shadow queries
-  double hp[3][256], nn[3][256], wo[3][256];
-  uint32_t bsdf[256];
-  float cr[256], cg[256], cb[256];  // a light sample's contribution, parked across its shadow query
-                                    // (the batch kernel's fold then reads each sample's radiance here)
+// per-lane LDS slots, structure-of-arrays (consecutive lanes hit consecutive banks), N lanes per block
+template <uint32_t N>
+struct ShadeLdsN {  // the camera hit being shaded, parked across its shadow queries
+  double hp[3][N], nn[3][N], wo[3][N];
+  uint32_t bsdf[N];
+  float cr[N], cg[N], cb[N];  // a light sample's contribution, parked across its shadow query
+                              // (the batch kernel's fold then reads each sample's radiance here)
 };
+using ShadeLds = ShadeLdsN<256>;
 struct ColdLds : ShadeLds {  // + the per-pixel sums of the lane-per-pixel kernel
   double s1[256], s2[256];
   float rr[256], rg[256], rb[256];
@@ -34,7 +36,8 @@ template <class T>
 __device__ __forceinline__ T lget(const T* a, uint32_t i) { return ((const volatile T*)a)[i]; }
 
 // park a camera-hit record in the lane's LDS slots
-__device__ __forceinline__ void park_hit(ShadeLds& cl, uint32_t t, const Isect& is0) {
+template <class SL>
+__device__ __forceinline__ void park_hit(SL& cl, uint32_t t, const Isect& is0) {
   for (int k = 0; k < 3; ++k) {
     lput(cl.hp[k], t, (&is0.hit_p.x)[k]);
     lput(cl.nn[k], t, (&is0.n.x)[k]);
@@ -46,8 +49,8 @@ __device__ __forceinline__ void park_hit(ShadeLds& cl, uint32_t t, const Isect& 
 // estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
 // W: the calling kernel build's tag for the out-of-line occlusion proof (rrt_device.h query_nx)
-template <bool COUNT, int LEAN, bool NI = false, int W = 0>
-__device__ spec direct_importance_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
+template <bool COUNT, int LEAN, bool NI = false, int W = 0, class SL = ShadeLds>
+__device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
   int total = 0;
@@ -115,6 +118,7 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 // cost it 10%, more than the proof saved) nor the Kerr builds (no planar recurrence).  One tag per
 // kernel build (batch kernels; per-sample kernels, counting or not).
 #define RRT_OCC_TAG(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 8 * (WAVES) + (LEAN) + 1 : 0)
+#define RRT_OCC_TAG_SLOT(LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 256 + 8 * (WAVES) + (LEAN) + 1 : 0)
 #define RRT_OCC_TAG_S(COUNT, LEAN, WAVES) ((LEAN) == 1 || (LEAN) == 0 ? 64 + ((COUNT) ? 128 : 0) + 8 * (WAVES) + (LEAN) + 1 : 0)
 
 #if RRT_PROFILE
@@ -131,6 +135,15 @@ extern "C" int rrt_prof_read_slow(unsigned long long* out) {  // out: 64; resets
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof_slow), sizeof(rrt_prof_slow)) != hipSuccess) return -1;
   unsigned long long z[64] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(rrt_prof_slow), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// per pixel slot (slot < 2^21, e.g. 1080p): elapsed wall ticks (claim to stop, 24 bits) << 8 | rounds
+__device__ uint32_t rrt_prof_px[1u << 21];
+extern "C" int rrt_prof_read_px(uint32_t* out, uint32_t n) {  // reads and resets min(n, 2^21) slots
+  n = n < (1u << 21) ? n : (1u << 21);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof_px), n * sizeof(uint32_t)) != hipSuccess) return -1;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(rrt_prof_px)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(uint32_t) << 21) == hipSuccess ? 0 : -1;
 }
 extern "C" int rrt_prof_read(unsigned long long* out) {  // out: RRT_PROF_HDR + 3 * 16384
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof), sizeof(rrt_prof)) != hipSuccess) return -1;
@@ -368,6 +381,87 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
   uint8_t sst[32][NSLOTS], sown[32][NSLOTS];
 };
 
+// Heavy pixel hx of the pixel proof pass's heavy list (rrt_device.h pixel_heavy),
+// rendered by one whole wave: the 64 consecutive draw-offset slots of a step in parallel.
+// Sample k of a pixel starts at draw offset Dm * m_k with m_0 = 0 and m_{k+1} = m_k + (hit_k ?
+// Dh / Dm : 1) (the slots below, counted from the pixel's first draw), so slot m's sample -- the
+// camera ray from its jitter draws, then est_radiance_global_illumination with the draws that
+// follow -- is the same whichever sample lands on it.  A step of up to samples_per_batch samples
+// spans at most (spb - 1) Dh / Dm + 1 <= 64 slots from its first (the host's condition), so one
+// round of the wave's lanes resolves the whole step: the chain follows from the ballot of hits,
+// and the samples on it are folded in sample order with the adaptive stop at the step's end
+// (raytrace_pixel, part1_code.cpp:136-158) -- the group leader's fold below, so the result is
+// the same.  The pixel takes one round per step instead of the speculation rounds (four to seven
+// for pixels that straddle the capture boundary).  Wave-uniform; t: the lane's ShadeLds slot.
+// Out of line, one copy per kernel build (W), so the batch kernel's group loop keeps its own
+// register allocation (inlined, the prologue raised the cfg3 build's spills 656 -> 768 B/lane).
+template <int LEAN, int W>
+__device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& cl, uint32_t t, uint32_t lane, uint32_t hx,
+                                                 rrt::Counters& cn) {
+  using namespace rrt;
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit, S1 = Dh / Dm;
+  const DCamera& cam = kp.cam;
+  const uint32_t ix = kp.heavy_list[hx];
+  const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+  const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
+  const uint64_t key = rrt_pixel_key(kp.seed, x, y);
+  spec ret = S(0, 0, 0);
+  double s1 = 0.0, s2 = 0.0;
+  uint32_t i = 0, m0 = 0;  // samples folded; the step's first slot
+  for (;;) {
+    const uint32_t sl = m0 + lane;
+    Rng g; g.key = key; g.ctr = sl * Dm;
+    double jx, jy; g.grid(jx, jy);  // Camera::generate_ray (part1_code.cpp:182-187) at the slot's jitter
+    const double sx = (double)x + jx, sy = (double)y + jy;
+    const double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
+    const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
+    const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+    const v3 wd = unit(w);
+    Isect is;
+    const bool hit = !camera_proven_miss<false, false>(kp, ld3(cam.pos), wd, cn) &&
+                     query_nx<false, false, RRT_BATCH_CALL, false>(kp, ld3(cam.pos), wd, &is, cn);
+    spec s = S(0, 0, 0);
+    if (hit) {
+      park_hit(cl, t, is);
+      g.ctr = sl * Dm + Dm;
+      const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
+      if (kp.max_ray_depth == 0) s = e;
+      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, W>(kp, g, cl, t, cn);
+    }
+    // the step's chain over the slots (wave-uniform) and the ordered fold
+    const uint64_t hits = __ballot(hit);
+    const uint32_t to_check = kp.samples_per_batch - i % kp.samples_per_batch;
+    const uint32_t left = min(kp.ns_aa - i, to_check);
+    uint32_t m = 0;  // slot relative to m0
+    for (uint32_t k = 0; k < left; ++k) {
+      const spec sk = S(__shfl(s.r, (int)m), __shfl(s.g, (int)m), __shfl(s.b, (int)m));
+      if (sk.r != 0.0f || sk.g != 0.0f || sk.b != 0.0f) {  // zero samples: identities on the sums
+        ret = ret + sk;
+        const double il = illum(sk);
+        s1 += il;
+        s2 += il * il;
+      }
+      m += ((hits >> m) & 1ull) ? S1 : 1u;
+    }
+    i += left;
+    m0 += m;
+    bool st = i >= kp.ns_aa;
+    if (i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
+      const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
+      if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
+    }
+    if (st) break;
+  }
+  if (lane == 0) {
+    const uint32_t slot = tl * tpix + r;
+    const spec rr = ret / (float)i;
+    kp.rgb[3 * slot] = rr.r; kp.rgb[3 * slot + 1] = rr.g; kp.rgb[3 * slot + 2] = rr.b;
+    kp.count[slot] = (int32_t)i;
+    if (kp.draws) kp.draws[slot] = m0 * Dm;
+  }
+}
+
 template <int LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
@@ -396,6 +490,31 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   uint32_t prof_blocks = 0, prof_samples = 0;  // pixels claimed, query rounds
   uint32_t px_rounds = 0, px_steps = 0;           // of the group's current pixel
 #endif
+
+  // Heavy pixels first (the pass's heavy list): the first waves to start take one each, whole
+  // wave per pixel, at issue priority 3 -- they are the frame's slowest pixels -- then join the
+  // group loop below
+  if (is_lean(LEAN) && kp.heavy_list) {  // (the pass runs for the LEAN builds only)
+    const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
+    for (;;) {
+      uint32_t k = 0;
+      if (lane == 0) k = atomicAdd(kp.heavy_count + 1, 1u);
+      k = __shfl(k, 0);
+      if (k >= nh) break;
+      __builtin_amdgcn_s_setprio(3);
+#if RRT_PROFILE
+      const uint64_t w_h = wall_clock64();
+#endif
+      heavy_pixel_wave<LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, cl, t, lane, k, cn);
+#if RRT_PROFILE  // elapsed ticks; "rounds" 1
+      if (lane == 0) {
+        const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + ix % tpix;
+        if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
+      }
+#endif
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
 
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
@@ -730,6 +849,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
           atomicMax(&rrt_prof_slow[slot & 63u], (el << 38) | ((unsigned long long)min(px_rounds, 127u) << 31) |
                                                     ((unsigned long long)min(px_steps, 127u) << 24) |
                                                     (unsigned long long)(slot & 0xffffffu));
+          if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(el, (uint64_t)0xffffff) << 8) | min(px_rounds, 255u);
         }
 #endif
         const spec r = ret / (float)i;
@@ -781,7 +901,7 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
   using namespace rrt;
   const uint32_t ix = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
-  bool listed = false;
+  bool listed = false, heavy = false;
   if (ix < kp.n_pixels) {
     const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
     const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
@@ -793,7 +913,20 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
         if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
       } else {
         listed = true;
+        heavy = kp.heavy_list && pixel_heavy(kp, x, y);
       }
+    }
+  }
+  // heavy pixels go to the slot kernel's list while it has room (the rest to the claim list)
+  const uint64_t hb = __ballot(heavy);
+  if (hb) {
+    uint32_t hbase = 0;
+    if (lane == 0) hbase = atomicAdd(kp.heavy_count, (uint32_t)__popcll(hb));
+    hbase = __shfl(hbase, 0);
+    const uint32_t k = hbase + (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
+    if (heavy && k < kp.heavy_cap) {
+      kp.heavy_list[k] = ix;
+      listed = false;
     }
   }
   // RRT_CLAIM_HYP 2: a listed pixel's hint bit (31) = its central camera ray is no proven miss
@@ -815,6 +948,7 @@ hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStr
   hipLaunchKernelGGL(rrt_pixel_proof_kernel, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_kp);
   return hipGetLastError();
 }
+
 
 // Sample 0 of every pixel, one lane per pixel (tile-list order, so a wave covers two rows of a
 // tile).  Its draw offset is always 0, so it needs no speculation; its hit status then seeds the

@@ -99,7 +99,10 @@ def test_kerr_differs_from_schwarzschild(gpu):
     assert np.array_equal(s_rgb.view(np.uint32), c.px["rgb"].view(np.uint32))
 
 
-def test_wavefront_rejects_kerr(gpu):
+def test_removed_wavefront_flag_is_rejected(gpu):
+    """The wavefront A/B kernel (round 1-2, slower in every measurement) is gone from the library;
+    its flag fails loudly instead of silently running another kernel."""
     c = Case("spheres_96x72_s1")
-    with pytest.raises(rrt.RRTError):
+    with pytest.raises(rrt.RRTError) as e:
         gpu_render(gpu, c, 0.5, (0.0, 1.0, 0.0), flags=rrt.RRT_RENDER_WAVEFRONT)
+    assert e.value.code == rrt.RRT_E_INVALID

@@ -56,7 +56,7 @@ def check(c, rgb, cnt, draws):
 
 # every kernel path must meet the same bar: default (sample-parallel kernel, clean-tree BVH walk,
 # empty-space grid), the reference-tree walk without the grid, the lane-per-pixel per-sample
-# kernel, the per-pixel-loop kernel and the wavefront state-machine kernel; the sample-parallel
+# kernel and the per-pixel-loop kernel; the sample-parallel
 # kernel also with one chip-wide claim queue, one queue per XCD, and in list order; and the
 # default path with every camera ray marched exactly (no miss proof) and with every shadow ray
 # marched exactly (no occlusion proof); at depth >= 2 also the per-sample refill kernel
@@ -65,17 +65,15 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
             "ordered": rrt.RRT_RENDER_ORDERED, "noproof": rrt.RRT_RENDER_NO_MISS_PROOF,
             "prepass": rrt.RRT_RENDER_PREPASS, "striped": rrt.RRT_RENDER_STRIPED_QUEUES,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
-            "wavefront": rrt.RRT_RENDER_WAVEFRONT, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
+            "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
             "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
-            "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE}
+            "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE, "noheavy": rrt.RRT_RENDER_NO_HEAVY}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("name", SMALL)
 def test_small_cases(gpu, name, variant):
     c = Case(name)
-    if variant == "wavefront" and c.envmap is not None:
-        pytest.skip("the wavefront A/B kernel has no environment-map path (rejected by the library)")
     rgb, cnt, draws, _ = render(gpu, c, flags=VARIANTS[variant])
     print(variant, end=" ")
     check(c, rgb, cnt, draws)
@@ -84,7 +82,8 @@ def test_small_cases(gpu, name, variant):
 PROOFS = {"proofs": 0,
           "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF | rrt.RRT_RENDER_NO_PIXEL_PROOF,
           "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
-          "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE}
+          "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
+          "noheavy": rrt.RRT_RENDER_NO_HEAVY}
 
 
 @pytest.mark.parametrize("proof", sorted(PROOFS))
@@ -96,6 +95,12 @@ def test_baseline_frames(gpu, name, proof):
     c = Case(name)
     rgb, cnt, draws, _ = render(gpu, c, flags=PROOFS[proof])
     check(c, rgb, cnt, draws)
+    heavy = gpu.stats().last_heavy_pixels
+    print("heavy pixels", heavy)
+    if name.startswith("cfg3") and proof == "proofs":  # the hole's capture ring: slot-parallel pixels
+        assert heavy > 0
+    if proof in ("noheavy", "nopixelproof", "noproofs") or name.startswith("cfg2"):  # no pass / flat
+        assert heavy == 0
 
 
 def test_work_counters_closest_hit(gpu):

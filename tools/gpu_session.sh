@@ -79,6 +79,18 @@ for step in "$@"; do
     abtree) run abtree3 600 python3 tools/ab_workload.py --workload cfg3 --rounds 3 0 0:262144 &&
             run abtree4 600 python3 tools/ab_workload.py --workload cfg4 --rounds 2 0 0:262144 &&
             run abtree5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 0:262144 ;;
+    heavy) # heavy-pixel slot path: parity (BASELINE frames + small cases), A/B on cfg3, per-pixel phase profile
+           run pytest_heavy 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "baseline or noheavy or bunny_B or spheres_B" &&
+           run abheavy 600 python3 tools/ab_workload.py --workload cfg3 --rounds 3 0 0:1048576 65536 196608 &&
+           run profheavy 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profheavy -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --rounds 2 0 0:1048576 &&
+           RRT_LIB=tools/_var/librrt_prof.so run phase3h 300 python3 tools/phase_profile.py --flags 0 ;;
+    profheavy) # per-kernel durations with and without the heavy path (cfg3)
+           run profheavy 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profheavy -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --rounds 2 0 0:1048576 ;;
+    phaseall) # phase profiles of cfg3 (frame + streak crop), cfg4 and cfg5 on the -DRRT_PROFILE=1 build (make prof)
+           RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
+           RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 &&
+           RRT_LIB=tools/_var/librrt_prof.so run phase4 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 &&
+           RRT_LIB=tools/_var/librrt_prof.so run phase5 600 python3 tools/phase_profile.py --workload cfg5 --flags 0 ;;
     phase) RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
            RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
     abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 2 0 2 4 0:16 0:131072 ;;

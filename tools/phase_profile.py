@@ -25,17 +25,37 @@ def main():
     ap.add_argument("--flags", type=int, nargs="+", default=[0, rrt.RRT_RENDER_NO_MISS_PROOF])
     ap.add_argument("--tiles", type=int, nargs="*", default=None, help="x y pairs of 32x32 tiles (default: all)")
     ap.add_argument("--region", type=int, nargs=4, default=None, help="x0 y0 w h: render only this region")
+    ap.add_argument("--workload", default=None, help="a bench.py workload (cfg2..cfg5, m3) instead of a golden case")
     a = ap.parse_args()
-    c = Case(a.case)
-    g = c.cfg
     L = rrt.lib()
     L.rrt_prof_read.argtypes = [C.c_void_p]
     L.rrt_prof_read_slow.argtypes = [C.c_void_p]
     r = rrt.Renderer(0)
-    r.set_scene(rrt.SceneFile(c.scene_path))
-    r.set_camera(rrt.load_camera(c.camera_path))
-    r.set_black_hole(g["bh"][:3], g["bh"][3], g["bh"][4])
-    tiles = rrt.partition_tiles(c.frame_w, c.frame_h, 32, 0, 1)
+    if a.workload:
+        # bench.py's own set-up of the workload (native ingest, generated scenes / sky, Kerr)
+        sys.path.insert(0, ROOT)
+        import tempfile
+        import bench
+        wl = bench.WORKLOADS[a.workload]
+        work = tempfile.mkdtemp()
+        scene, cam, _, _ = bench.load_workload_scene(wl, work)
+        r.set_scene(scene)
+        r.set_camera(rrt.camera_desc(cam))
+        r.set_envmap(bench.load_workload_env(wl, work))
+        kerr = wl.get("kerr")
+        r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
+        frame_w, frame_h = wl["w"], wl["h"]
+        g = dict(ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), ns_area_light=1, samples_per_batch=32,
+                 max_tolerance=0.05, direct_hemisphere=False)
+        a.case = a.workload
+    else:
+        c = Case(a.case)
+        g = c.cfg
+        r.set_scene(rrt.SceneFile(c.scene_path))
+        r.set_camera(rrt.load_camera(c.camera_path))
+        r.set_black_hole(g["bh"][:3], g["bh"][3], g["bh"][4])
+        frame_w, frame_h = c.frame_w, c.frame_h
+    tiles = rrt.partition_tiles(frame_w, frame_h, 32, 0, 1)
     if a.tiles:
         tiles = np.array(a.tiles, np.uint32).reshape(-1, 2)
     n = len(tiles) * 1024
@@ -45,7 +65,7 @@ def main():
     buf = np.zeros(HDR + 3 * 16384, np.uint64)
     out = {}
     for fl in a.flags:
-        p = rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+        p = rrt.render_params(frame_w, frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
                               ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
                               max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=fl)
         L.rrt_prof_read(buf.ctypes.data)
@@ -66,6 +86,19 @@ def main():
         blocks, samples = (work >> np.uint64(32)).astype(np.int64), (work & np.uint64(0xffffffff)).astype(np.int64)
         res = blocks > 0
         np.savez(f"gpurun_out/waves_{fl}.npz", ends=ends, starts=starts, blocks=blocks, samples=samples)
+        if not a.region and n <= (1 << 21):  # per-pixel elapsed ticks and rounds (batch kernel)
+            L.rrt_prof_read_px.argtypes = [C.c_void_p, C.c_uint32]
+            pxv = np.zeros(n, np.uint32)
+            L.rrt_prof_read_px(pxv.ctypes.data, n)
+            img_t = np.zeros((frame_h, frame_w), np.float32)
+            img_r = np.zeros((frame_h, frame_w), np.uint8)
+            sl = np.arange(n)
+            xs = tiles[sl // 1024, 0].astype(np.int64) + sl % 1024 % 32
+            ys = tiles[sl // 1024, 1].astype(np.int64) + sl % 1024 // 32
+            ok = (xs < frame_w) & (ys < frame_h)
+            img_t[ys[ok], xs[ok]] = (pxv[ok] >> 8) / (span / ms)
+            img_r[ys[ok], xs[ok]] = pxv[ok] & 255
+            np.savez_compressed(f"gpurun_out/px_{a.case}_{fl}.npz", ms=img_t, rounds=img_r)
         slow = np.zeros(64, np.uint64)
         L.rrt_prof_read_slow(slow.ctypes.data)
         slow_px = []
