@@ -160,7 +160,11 @@ typedef struct {
                                  depth<=1 kernel is built for (1..6, register budget); bits
                                  8..11: the sample-0 pre-pass's waves/SIMD; bits 16..19: the heavy-pixel
                                  threshold (1: capture boundary only; 2 / 3 / 4: rays within
-                                 1.1 / 1.5 / 2.0 r_s; 0: 1.2) */
+                                 1.1 / 1.5 / 2.0 r_s; 0: 1.2); bits 12..15: blocks per CU the
+                                 batch grid leaves free besides the heavy kernel's; bit 23: no
+                                 room left for the heavy kernel; bits 24..27: the heavy-pixel
+                                 kernel's waves/SIMD (2..5; 0: 4); bits 28..31: its grid in
+                                 quarters of the CU count (0: 1) */
 } rrt_render_params;
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
@@ -207,6 +211,10 @@ enum {
   RRT_RENDER_NO_HEAVY = 1u << 20, /* sample-parallel kernel: no slot-parallel path for heavy
                                      pixels (those whose rays straddle the hole's capture boundary
                                      or pass close to it; A/B and parity, results are identical) */
+  RRT_RENDER_HEAVY = 1u << 21,    /* sample-parallel kernel: the heavy pixels' path also for a
+                                     launch covering most of the frame (by default it runs only
+                                     for launches of at most 60% of the frame's pixels, e.g. one
+                                     rank's tiles of a multi-GPU frame; results are identical) */
   RRT_RENDER_DEEP_SAMPLE = 1u << 19, /* depth >= 2 (Schwarzschild): the per-sample refill kernel
                                      instead of the per-pixel loop (A/B; results are identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes

@@ -27,6 +27,7 @@ hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, 
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream);
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -99,6 +100,8 @@ struct rrt_ctx {
   // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
   uint32_t* d_heavy_list = nullptr;
   size_t heavy_list_cap = 0;
+  hipStream_t side = nullptr;  // the heavy pixels' kernel runs here, beside the batch kernel
+  hipEvent_t ev_go = nullptr, ev_heavy = nullptr;
   bool fenced = false;
   int n_cu = 256;
   // host scene
@@ -199,6 +202,15 @@ static void free_scene_dev(rrt_ctx* c) {
 }
 
 
+// The heavy pixels' stream: a high-priority stream, on a hardware queue of its own, so its kernel
+// runs beside the batch kernel (a CU-masked stream ran it behind the batch kernel: cfg3 23.9 ms
+// against 19.4 ms for a plain or a high-priority stream).
+static bool create_side_stream(rrt_ctx* c) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+  return hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) == hipSuccess;
+}
+
 static bool create_ring(rrt_ctx* c) {
   for (uint32_t i = 0; i < rrt_ctx::kRing; ++i)
     if (hipEventCreate(&c->ev0[i]) != hipSuccess || hipEventCreate(&c->ev_main[i]) != hipSuccess ||
@@ -228,6 +240,9 @@ int rrt_create(rrt_ctx** out, const rrt_device_cfg* cfg) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         !create_ring(c.get()) ||
         hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming) != hipSuccess ||
+        !create_side_stream(c.get()) ||
+        hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming) != hipSuccess ||
 
         hipMalloc(&c->d_counter, kCounterBytes) != hipSuccess || hipMalloc(&c->d_kp, sizeof(KParams)) != hipSuccess) {
       *out = nullptr;
@@ -254,6 +269,9 @@ void rrt_destroy(rrt_ctx* c) {
       if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
     }
     if (c->ev_fence) hipEventDestroy(c->ev_fence);
+    if (c->ev_go) hipEventDestroy(c->ev_go);
+    if (c->ev_heavy) hipEventDestroy(c->ev_heavy);
+    if (c->side) hipStreamDestroy(c->side);
     if (c->stream) hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1386,7 +1404,13 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       // heavy_pixel_wave); needs a hit to take a whole number of slots (Dh = k Dm) and a step's
       // chain to fit the wave's 64 slots
       const uint32_t spb = std::min(p->samples_per_batch, p->ns_aa);
-      if (!(p->flags & RRT_RENDER_NO_HEAVY) && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 &&
+      // Only for launches covering at most 60% of the frame (one rank's tiles of a multi-GPU
+      // frame, the regions of the host path): there the heavy pixels' latency bounds the launch
+      // (cfg3 split 8 ways, slowest rank 7.6 -> 5.5 ms); a whole frame is bound by its throughput,
+      // and the heavy kernel's room in the batch grid costs more than it saves (18.2 -> 19.2 ms)
+      const uint64_t frame_px = (uint64_t)p->frame_w * p->frame_h;
+      const bool share_ok = (p->flags & RRT_RENDER_HEAVY) || (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
+      if (!(p->flags & RRT_RENDER_NO_HEAVY) && share_ok && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 &&
           (spb - 1) * (kp.draws_hit / kp.draws_miss) + 1 <= 64u) {
         // at most 1/256 of the pixels (4096 at least): a frame mostly near the hole stays with
         // the batch kernel, whose rounds cost less than 64 slots a step for unmixed pixels
@@ -1472,7 +1496,26 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
                                  stream));
     if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
-    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, grid, stream));
+    uint32_t bgrid = grid;
+    if (kp.heavy_list) {
+      // the heavy pixels' kernel (rrt_sample.hip rrt_heavy_kernel) on the side stream (its own
+      // hardware queue), after the pass, beside the batch kernel; the batch grid leaves room for
+      // its blocks (one per CU at most, <= 128 VGPRs and 23 KB of LDS next to four batch blocks),
+      // whichever kernel the hardware dispatches first
+      const uint32_t hwv = (p->variant >> 24) & 0xfu, hgv = (p->variant >> 28) & 0xfu;
+      const int hw = (hwv >= 2 && hwv <= 5) ? (int)hwv : 4;
+      const uint32_t hgrid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 1u) / 4u, (uint32_t)c->n_cu));
+      const uint32_t resident = (uint32_t)c->n_cu * (uint32_t)(lean == 1 || lean == 2 ? w : gw);  // blocks of 4 waves
+      const uint32_t spare = ((p->variant >> 12) & 0xfu) * (uint32_t)c->n_cu;  // A/B: more room (blocks per CU)
+      const bool no_room = (p->variant >> 23) & 1u;  // A/B: leave the batch grid as it is
+      if (!no_room && bgrid + hgrid + spare > resident) bgrid = resident > hgrid + spare ? resident - hgrid - spare : 1u;
+      HIPCHK(c, hipEventRecord(c->ev_go, stream));
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
+      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, hgrid, c->side));
+      HIPCHK(c, hipEventRecord(c->ev_heavy, c->side));
+    }
+    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, bgrid, stream));
+    if (kp.heavy_list) HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   tf[deep], tf[count], lean == 2 ? 0 : lean);

@@ -195,8 +195,8 @@ struct KParams {
   uint32_t* draws;      // optional
   uint32_t* counters;   // optional [4] per pixel
   DShadowProof occ;     // the hot fields above keep their offsets
-  // heavy pixels (rrt_pixel_proof_kernel pixel_heavy -> rrt_batch_kernel heavy_pixel_wave): listed
-  // pixels rendered slot-parallel, one wave per pixel and a step's 64 draw-offset slots per round
+  // heavy pixels (rrt_pixel_proof_kernel pixel_heavy -> rrt_heavy_kernel): listed pixels rendered
+  // slot-parallel, one wave per pixel and a step's 64 draw-offset slots per round
   uint32_t* heavy_list;   // claim indices (null: no heavy path)
   uint32_t* heavy_count;  // [0]: entries appended by the pass (capped at heavy_cap); [1]: entries taken
   uint32_t heavy_cap;     // list capacity

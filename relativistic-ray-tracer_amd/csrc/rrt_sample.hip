@@ -393,8 +393,11 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
 // (raytrace_pixel, part1_code.cpp:136-158) -- the group leader's fold below, so the result is
 // the same.  The pixel takes one round per step instead of the speculation rounds (four to seven
 // for pixels that straddle the capture boundary).  Wave-uniform; t: the lane's ShadeLds slot.
-// Out of line, one copy per kernel build (W), so the batch kernel's group loop keeps its own
-// register allocation (inlined, the prologue raised the cfg3 build's spills 656 -> 768 B/lane).
+// It runs in a kernel of its own (rrt_heavy_kernel), so neither register allocation constrains
+// the other: called out of line from the batch kernel, it had doubled the group loop's spills
+// (cfg3 batch kernel 17.3 -> 33.5 ms).  Out of line there too: inlined into the batch kernel,
+// the build hung on the first heavy pixel of bunny_B1_160x120_s16, while the out-of-line build
+// renders it bit-exactly (tools/probe_case.py; cause not found).
 template <int LEAN, int W>
 __device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& cl, uint32_t t, uint32_t lane, uint32_t hx,
                                                  rrt::Counters& cn) {
@@ -462,6 +465,55 @@ __device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& 
   }
 }
 
+// The heavy pixels' kernel (heavy pixels), launched after the pixel proof pass on
+// the context's side stream -- a queue of its own -- beside the batch kernel, which leaves room
+// for its blocks (rrt_host.cpp): each wave takes heavy pixels one at a time, at issue priority 3.
+template <int LEAN, int HW>
+__global__ __launch_bounds__(256, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
+  using namespace rrt;
+  __shared__ ShadeLds cl;
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  Counters cn = {};
+  const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
+  __builtin_amdgcn_s_setprio(3);
+  for (;;) {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(kp.heavy_count + 1, 1u);
+    k = __shfl(k, 0);
+    if (k >= nh) break;
+#if RRT_PROFILE
+    const uint64_t w_h = wall_clock64();
+#endif
+    heavy_pixel_wave<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW)>(kp, cl, t, lane, k, cn);
+#if RRT_PROFILE  // elapsed ticks; "rounds" 1
+    if (lane == 0) {
+      const uint32_t ts = kp.tile_size, tpix = ts * ts;
+      const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + ix % tpix;
+      if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
+    }
+#endif
+  }
+}
+
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
+#define RRT_LAUNCH_H(L, W) hipLaunchKernelGGL((rrt_heavy_kernel<L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
+  if (lean == 1) {
+    switch (waves) {
+      case 2: RRT_LAUNCH_H(1, 2); break;
+      case 3: RRT_LAUNCH_H(1, 3); break;
+      case 5: RRT_LAUNCH_H(1, 5); break;
+      default: RRT_LAUNCH_H(1, 4); break;
+    }
+  } else if (lean == 2) {
+    RRT_LAUNCH_H(2, 4);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef RRT_LAUNCH_H
+  return hipGetLastError();
+}
+
 template <int LEAN, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
@@ -490,31 +542,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   uint32_t prof_blocks = 0, prof_samples = 0;  // pixels claimed, query rounds
   uint32_t px_rounds = 0, px_steps = 0;           // of the group's current pixel
 #endif
-
-  // Heavy pixels first (the pass's heavy list): the first waves to start take one each, whole
-  // wave per pixel, at issue priority 3 -- they are the frame's slowest pixels -- then join the
-  // group loop below
-  if (is_lean(LEAN) && kp.heavy_list) {  // (the pass runs for the LEAN builds only)
-    const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
-    for (;;) {
-      uint32_t k = 0;
-      if (lane == 0) k = atomicAdd(kp.heavy_count + 1, 1u);
-      k = __shfl(k, 0);
-      if (k >= nh) break;
-      __builtin_amdgcn_s_setprio(3);
-#if RRT_PROFILE
-      const uint64_t w_h = wall_clock64();
-#endif
-      heavy_pixel_wave<LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, cl, t, lane, k, cn);
-#if RRT_PROFILE  // elapsed ticks; "rounds" 1
-      if (lane == 0) {
-        const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + ix % tpix;
-        if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
-      }
-#endif
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
 
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)

@@ -26,7 +26,7 @@ RRT_RENDER_PIXEL_LOOP, RRT_RENDER_NO_SKIP, RRT_RENDER_NO_CLEAN, RRT_RENDER_PER_P
 RRT_RENDER_COUNT_EXECUTED, RRT_RENDER_ORDERED, RRT_RENDER_NO_FIRST = 256, 512, 1024
 RRT_RENDER_ONE_QUEUE, RRT_RENDER_XCD_QUEUES, RRT_RENDER_NO_MISS_PROOF, RRT_RENDER_PREPASS = 2048, 4096, 8192, 16384
 RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF, RRT_RENDER_NO_PIXEL_PROOF = 1 << 15, 1 << 16, 1 << 17
-RRT_RENDER_NO_SEARCH_TREE, RRT_RENDER_DEEP_SAMPLE, RRT_RENDER_NO_HEAVY = 1 << 18, 1 << 19, 1 << 20
+RRT_RENDER_NO_SEARCH_TREE, RRT_RENDER_DEEP_SAMPLE, RRT_RENDER_NO_HEAVY, RRT_RENDER_HEAVY = 1 << 18, 1 << 19, 1 << 20, 1 << 21
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
 
 

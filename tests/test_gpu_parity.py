@@ -67,7 +67,8 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
             "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
             "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
-            "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE, "noheavy": rrt.RRT_RENDER_NO_HEAVY}
+            "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE, "noheavy": rrt.RRT_RENDER_NO_HEAVY,
+            "heavy": rrt.RRT_RENDER_HEAVY}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -83,7 +84,7 @@ PROOFS = {"proofs": 0,
           "noproofs": rrt.RRT_RENDER_NO_MISS_PROOF | rrt.RRT_RENDER_NO_SHADOW_PROOF | rrt.RRT_RENDER_NO_PIXEL_PROOF,
           "nocamproof": rrt.RRT_RENDER_NO_MISS_PROOF, "noshadowproof": rrt.RRT_RENDER_NO_SHADOW_PROOF,
           "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
-          "noheavy": rrt.RRT_RENDER_NO_HEAVY}
+          "noheavy": rrt.RRT_RENDER_NO_HEAVY, "heavy": rrt.RRT_RENDER_HEAVY}
 
 
 @pytest.mark.parametrize("proof", sorted(PROOFS))
@@ -97,9 +98,10 @@ def test_baseline_frames(gpu, name, proof):
     check(c, rgb, cnt, draws)
     heavy = gpu.stats().last_heavy_pixels
     print("heavy pixels", heavy)
-    if name.startswith("cfg3") and proof == "proofs":  # the hole's capture ring: slot-parallel pixels
+    if name.startswith("cfg3") and proof == "heavy":  # the hole's capture ring: slot-parallel pixels
         assert heavy > 0
-    if proof in ("noheavy", "nopixelproof", "noproofs") or name.startswith("cfg2"):  # no pass / flat
+    # no pass / flat / a whole frame (the heavy path runs by default for launches of <= 60% of it)
+    if proof in ("noheavy", "nopixelproof", "noproofs", "proofs") or name.startswith("cfg2"):
         assert heavy == 0
 
 
@@ -137,6 +139,43 @@ def test_device_tiles_path_matches_host_path(gpu):
         torch.cuda.synchronize()
         assert np.array_equal(out_rgb.cpu().numpy().reshape(H, W, 3).view(np.uint32), rgb_h.view(np.uint32))
         assert np.array_equal(out_cnt.cpu().numpy().reshape(H, W), cnt_h)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_rank_tiles_cfg3_heavy_path(gpu, world):
+    """Every rank's tile set of the cfg3 frame (bench.py's block-cyclic split over `world` GPUs),
+    rendered on this GPU through the device path, unpacked into one frame: bit-exact against the
+    reference's frame.  A rank's launch covers <= 60% of the frame, so the heavy pixels' kernel
+    runs beside the batch kernel (its pixels straddle the hole's capture ring)."""
+    torch = pytest.importorskip("torch")
+    c = Case("cfg3_bunny_1080p_s64")
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(c.envmap)
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    bh = c.cfg["bh"]
+    gpu.set_black_hole(bh[:3], bh[3], bh[4])
+    W, H, ts, g = c.frame_w, c.frame_h, 32, c.cfg
+    p = rrt.render_params(W, H, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"], ns_area_light=g["ns_area_light"],
+                          samples_per_batch=g["samples_per_batch"], max_tolerance=g["max_tolerance"])
+    out_rgb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    out_cnt = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    heavy = 0
+    for r in range(world):
+        tiles = rrt.partition_tiles(W, H, ts, r, world)
+        prgb = torch.zeros(len(tiles) * ts * ts * 3, dtype=torch.float32, device="cuda")
+        pcnt = torch.zeros(len(tiles) * ts * ts, dtype=torch.int32, device="cuda")
+        gpu.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        heavy += gpu.stats().last_heavy_pixels
+        gpu.unpack_tiles_device(tiles, ts, W, H, prgb.data_ptr(), pcnt.data_ptr(), out_rgb.data_ptr(),
+                                out_cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    print("world", world, "heavy pixels", heavy)
+    assert heavy > 0
+    rgb = out_rgb.cpu().numpy().reshape(H, W, 3)
+    assert np.array_equal(rgb.view(np.uint32), c.px["rgb"].view(np.uint32))
+    assert np.array_equal(out_cnt.cpu().numpy().reshape(H, W), c.px["count"])
 
 
 def test_tonemap(gpu):

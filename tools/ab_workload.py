@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B kernel variants (rrt_render_params.variant = waves per SIMD, flags) on a bench.py workload,
 interleaved rounds in one process; prints the HIP-event kernel time per variant.
-Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT or VARIANT:FLAGS)"""
+Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT or VARIANT:FLAGS)
+--world N: time each of the N ranks' tile sets (bench.py's block-cyclic split) on this one GPU and
+report the slowest rank per variant (the N-GPU frame's kernel time, without the gather)."""
 import argparse
 import json
 import os
@@ -21,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg5", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--world", type=int, default=1)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
@@ -33,24 +36,35 @@ def main():
     r.set_envmap(bench.load_workload_env(wl, work))
     kerr = wl.get("kerr")
     r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
-    tiles = rrt.partition_tiles(W, H, ts, 0, 1)
-    n = len(tiles) * ts * ts
+    sets = [rrt.partition_tiles(W, H, ts, k, a.world) for k in range(a.world)]
+    n = max(len(t) for t in sets) * ts * ts
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     times, sums = {v: [] for v in a.variants}, {}
+    per_rank = {v: [[] for _ in sets] for v in a.variants}
     for _ in range(a.rounds):
         for v in a.variants:
             var, _, fl = v.partition(":")
             p = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), variant=int(var), flags=int(fl or 0))
-            r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
-            torch.cuda.synchronize()
-            times[v].append(r.stats().last_kernel_ms)
-            sums[v] = (float(prgb.double().sum().item()), int(pcnt.long().sum().item()))
+            worst, tot_rgb, tot_cnt = 0.0, 0.0, 0
+            for k, tiles in enumerate(sets):
+                r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+                torch.cuda.synchronize()
+                ms = r.stats().last_kernel_ms
+                per_rank[v][k].append(ms)
+                worst = max(worst, ms)
+                m = len(tiles) * ts * ts
+                tot_rgb += float(prgb[:3 * m].double().sum().item())
+                tot_cnt += int(pcnt[:m].long().sum().item())
+            times[v].append(worst)
+            sums[v] = (tot_rgb, tot_cnt)
             print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
     same = len(set(s for v, s in sums.items() if ":" not in v)) <= 1  # diagnostic flags change outputs
     print(json.dumps({"workload": a.workload, "identical_outputs": same,
                       "median_ms": {v: float(np.median(t)) for v, t in times.items()},
+                      **({"world": a.world, "rank_median_ms": {v: [float(np.median(x)) for x in pr] for v, pr in per_rank.items()}}
+                         if a.world > 1 else {}),
                       "sums": {v: list(x) for v, x in sums.items()}}))
 
 
