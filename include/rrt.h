@@ -161,10 +161,11 @@ typedef struct {
                                  8..11: the sample-0 pre-pass's waves/SIMD; bits 16..19: the heavy-pixel
                                  threshold (1: capture boundary only; 2 / 3 / 4: rays within
                                  1.1 / 1.5 / 2.0 r_s; 0: 1.2); bits 12..15: blocks per CU the
-                                 batch grid leaves free besides the heavy kernel's; bit 23: no
-                                 room left for the heavy kernel; bits 24..27: the heavy-pixel
-                                 kernel's waves/SIMD (2..5; 0: 4); bits 28..31: its grid in
-                                 quarters of the CU count (0: 1) */
+                                 batch grid leaves free besides the heavy kernel's; bits 20..21:
+                                 waves per heavy pixel (0: 2, 1: 1, 2: 4); bit 23: no room left
+                                 for the heavy kernel; bits 24..27: the heavy-pixel kernel's
+                                 waves/SIMD (4 or 5; 0: 4); bits 28..31: its waves in multiples
+                                 of the CU count (0: 2) */
 } rrt_render_params;
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */

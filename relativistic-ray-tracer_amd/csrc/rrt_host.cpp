@@ -27,7 +27,7 @@ hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, 
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream);
-hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
@@ -37,7 +37,7 @@ namespace {
 
 constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
 constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);  // claim counters + the pixel proof's list length + the heavy list's
-// Heavy pixels (rrt_sample.hip heavy_pixel_wave): rays passing within RRT_HEAVY_NEAR r_s of the hole (or straddling
+// Heavy pixels (rrt_sample.hip heavy_pixel_block): rays passing within RRT_HEAVY_NEAR r_s of the hole (or straddling
 // its capture boundary) make a pixel heavy (profiles/r03_heavy_ab.md)
 #define RRT_HEAVY_NEAR 1.2
 
@@ -1399,19 +1399,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       }
       kp.claim_list = c->d_list;
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
-      // Heavy pixels (rrt_device.h pixel_heavy): the pass lists them apart and the batch kernel's
-      // first waves render them slot-parallel, a whole wave per pixel (rrt_sample.hip
-      // heavy_pixel_wave); needs a hit to take a whole number of slots (Dh = k Dm) and a step's
-      // chain to fit the wave's 64 slots
-      const uint32_t spb = std::min(p->samples_per_batch, p->ns_aa);
+      // Heavy pixels (rrt_device.h pixel_heavy): the pass lists them apart and rrt_heavy_kernel
+      // renders them slot-parallel, a block of waves per pixel (rrt_sample.hip
+      // heavy_pixel_block); needs a hit to take a whole number of slots (Dh = k Dm)
       // Only for launches covering at most 60% of the frame (one rank's tiles of a multi-GPU
       // frame, the regions of the host path): there the heavy pixels' latency bounds the launch
       // (cfg3 split 8 ways, slowest rank 7.6 -> 5.5 ms); a whole frame is bound by its throughput,
       // and the heavy kernel's room in the batch grid costs more than it saves (18.2 -> 19.2 ms)
       const uint64_t frame_px = (uint64_t)p->frame_w * p->frame_h;
       const bool share_ok = (p->flags & RRT_RENDER_HEAVY) || (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
-      if (!(p->flags & RRT_RENDER_NO_HEAVY) && share_ok && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 &&
-          (spb - 1) * (kp.draws_hit / kp.draws_miss) + 1 <= 64u) {
+      if (!(p->flags & RRT_RENDER_NO_HEAVY) && share_ok && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0) {
         // at most 1/256 of the pixels (4096 at least): a frame mostly near the hole stays with
         // the batch kernel, whose rounds cost less than 64 slots a step for unmixed pixels
         const uint32_t cap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
@@ -1502,16 +1499,19 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       // hardware queue), after the pass, beside the batch kernel; the batch grid leaves room for
       // its blocks (one per CU at most, <= 128 VGPRs and 23 KB of LDS next to four batch blocks),
       // whichever kernel the hardware dispatches first
-      const uint32_t hwv = (p->variant >> 24) & 0xfu, hgv = (p->variant >> 28) & 0xfu;
-      const int hw = (hwv >= 2 && hwv <= 5) ? (int)hwv : 4;
-      const uint32_t hgrid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 1u) / 4u, (uint32_t)c->n_cu));
+      const uint32_t hwv = (p->variant >> 24) & 0xfu, hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
+      const int hw = hwv == 5 ? 5 : 4;
+      const int nw = (lean == 2 || nwv == 0) ? 2 : nwv == 1 ? 1 : 4;  // waves per heavy pixel
+      // heavy waves: hgv x the CU count (default 2), in blocks of nw waves
+      const uint32_t hwaves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
+      const uint32_t hgrid = std::max<uint32_t>(1u, hwaves / (uint32_t)nw);
       const uint32_t resident = (uint32_t)c->n_cu * (uint32_t)(lean == 1 || lean == 2 ? w : gw);  // blocks of 4 waves
-      const uint32_t spare = ((p->variant >> 12) & 0xfu) * (uint32_t)c->n_cu;  // A/B: more room (blocks per CU)
+      const uint32_t spare = ((p->variant >> 12) & 0xfu) * (uint32_t)c->n_cu + (hwaves + 3u) / 4u;  // room, in batch blocks
       const bool no_room = (p->variant >> 23) & 1u;  // A/B: leave the batch grid as it is
-      if (!no_room && bgrid + hgrid + spare > resident) bgrid = resident > hgrid + spare ? resident - hgrid - spare : 1u;
+      if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
       HIPCHK(c, hipEventRecord(c->ev_go, stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
-      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, hgrid, c->side));
+      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, nw, hgrid, c->side));
       HIPCHK(c, hipEventRecord(c->ev_heavy, c->side));
     }
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, bgrid, stream));

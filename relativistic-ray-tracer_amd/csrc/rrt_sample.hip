@@ -382,26 +382,33 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
 };
 
 // Heavy pixel hx of the pixel proof pass's heavy list (rrt_device.h pixel_heavy),
-// rendered by one whole wave: the 64 consecutive draw-offset slots of a step in parallel.
-// Sample k of a pixel starts at draw offset Dm * m_k with m_0 = 0 and m_{k+1} = m_k + (hit_k ?
-// Dh / Dm : 1) (the slots below, counted from the pixel's first draw), so slot m's sample -- the
-// camera ray from its jitter draws, then est_radiance_global_illumination with the draws that
-// follow -- is the same whichever sample lands on it.  A step of up to samples_per_batch samples
-// spans at most (spb - 1) Dh / Dm + 1 <= 64 slots from its first (the host's condition), so one
-// round of the wave's lanes resolves the whole step: the chain follows from the ballot of hits,
-// and the samples on it are folded in sample order with the adaptive stop at the step's end
-// (raytrace_pixel, part1_code.cpp:136-158) -- the group leader's fold below, so the result is
-// the same.  The pixel takes one round per step instead of the speculation rounds (four to seven
-// for pixels that straddle the capture boundary).  Wave-uniform; t: the lane's ShadeLds slot.
-// It runs in a kernel of its own (rrt_heavy_kernel), so neither register allocation constrains
-// the other: called out of line from the batch kernel, it had doubled the group loop's spills
-// (cfg3 batch kernel 17.3 -> 33.5 ms).  Out of line there too: inlined into the batch kernel,
-// the build hung on the first heavy pixel of bunny_B1_160x120_s16, while the out-of-line build
-// renders it bit-exactly (tools/probe_case.py; cause not found).
-template <int LEAN, int W>
-__device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& cl, uint32_t t, uint32_t lane, uint32_t hx,
-                                                 rrt::Counters& cn) {
+// rendered by one block of NW waves: its 64 NW consecutive draw-offset slots per round, in
+// parallel.  Sample k of a pixel starts at draw offset Dm * m_k with m_0 = 0 and m_{k+1} = m_k +
+// (hit_k ? Dh / Dm : 1) (the slots below, counted from the pixel's first draw), so slot m's
+// sample -- the camera ray from its jitter draws, then est_radiance_global_illumination with the
+// draws that follow -- is the same whichever sample lands on it.  After a round the block folds
+// the chain of samples over the computed slots in sample order, with the adaptive stop at each
+// step's end (raytrace_pixel, part1_code.cpp:136-158; the batch kernel's group-leader fold, so the
+// result is the same), and the next round starts at the first slot the chain has not reached.
+// With 128 slots a 64-sample pixel (two 32-sample steps, a hit taking two slots) takes one round,
+// where the batch kernel's speculation takes four to seven (pixels that straddle the capture
+// boundary).  Every thread runs the fold on the same LDS values, so control stays block-uniform.
+// The body stays out of line: inlined into the batch kernel, an earlier (per-wave) form of it hung
+// on the first heavy pixel of bunny_B1_160x120_s16 while the out-of-line build rendered it
+// bit-exactly (tools/probe_case.py; cause not found); called out of line from the batch kernel,
+// it doubled the group loop's spills (cfg3 batch kernel 17.3 -> 33.5 ms), hence its own kernel.
+template <int NW>
+struct HeavyLds {
+  rrt::ShadeLdsN<64 * NW> sh;  // parked hit records (direct_importance_parked)
+  float r[64 * NW], g[64 * NW], b[64 * NW];  // each slot's sample radiance
+  uint64_t hits[NW];  // each wave's ballot of hits
+  uint32_t hx;        // the claimed heavy-list entry
+};
+template <int LEAN, int W, int NW>
+__device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& hl, uint32_t t, uint32_t hx,
+                                               rrt::Counters& cn) {
   using namespace rrt;
+  constexpr uint32_t NS = 64u * NW;  // slots per round
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit, S1 = Dh / Dm;
   const DCamera& cam = kp.cam;
@@ -411,9 +418,9 @@ __device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& 
   const uint64_t key = rrt_pixel_key(kp.seed, x, y);
   spec ret = S(0, 0, 0);
   double s1 = 0.0, s2 = 0.0;
-  uint32_t i = 0, m0 = 0;  // samples folded; the step's first slot
+  uint32_t i = 0, m0 = 0;  // samples folded; the round's first slot
   for (;;) {
-    const uint32_t sl = m0 + lane;
+    const uint32_t sl = m0 + t;
     Rng g; g.key = key; g.ctr = sl * Dm;
     double jx, jy; g.grid(jx, jy);  // Camera::generate_ray (part1_code.cpp:182-187) at the slot's jitter
     const double sx = (double)x + jx, sy = (double)y + jy;
@@ -426,37 +433,41 @@ __device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& 
                      query_nx<false, false, RRT_BATCH_CALL, false>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (hit) {
-      park_hit(cl, t, is);
+      park_hit(hl.sh, t, is);
       g.ctr = sl * Dm + Dm;
-      const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
+      const spec e = emission(kp.bsdfs[lget(hl.sh.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, W>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, W>(kp, g, hl.sh, t, cn);
     }
-    // the step's chain over the slots (wave-uniform) and the ordered fold
-    const uint64_t hits = __ballot(hit);
-    const uint32_t to_check = kp.samples_per_batch - i % kp.samples_per_batch;
-    const uint32_t left = min(kp.ns_aa - i, to_check);
+    const uint64_t hb = __ballot(hit);
+    if ((t & 63u) == 0) hl.hits[t >> 6] = hb;
+    hl.r[t] = s.r; hl.g[t] = s.g; hl.b[t] = s.b;
+    __syncthreads();
+    // the chain over the computed slots and the ordered fold (every thread alike)
     uint32_t m = 0;  // slot relative to m0
-    for (uint32_t k = 0; k < left; ++k) {
-      const spec sk = S(__shfl(s.r, (int)m), __shfl(s.g, (int)m), __shfl(s.b, (int)m));
+    bool st = false;
+    while (m < NS) {
+      const spec sk = S(hl.r[m], hl.g[m], hl.b[m]);
       if (sk.r != 0.0f || sk.g != 0.0f || sk.b != 0.0f) {  // zero samples: identities on the sums
         ret = ret + sk;
         const double il = illum(sk);
         s1 += il;
         s2 += il * il;
       }
-      m += ((hits >> m) & 1ull) ? S1 : 1u;
+      ++i;
+      m += ((hl.hits[m >> 6] >> (m & 63u)) & 1ull) ? S1 : 1u;
+      st = i >= kp.ns_aa;
+      if (i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
+        const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
+        if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
+      }
+      if (st) break;
     }
-    i += left;
     m0 += m;
-    bool st = i >= kp.ns_aa;
-    if (i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
-      const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
-      if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
-    }
+    __syncthreads();  // the fold's reads before the next round's writes
     if (st) break;
   }
-  if (lane == 0) {
+  if (t == 0) {
     const uint32_t slot = tl * tpix + r;
     const spec rr = ret / (float)i;
     kp.rgb[3 * slot] = rr.r; kp.rgb[3 * slot + 1] = rr.g; kp.rgb[3 * slot + 2] = rr.b;
@@ -466,28 +477,30 @@ __device__ __noinline__ void heavy_pixel_wave(const KParams& kp, rrt::ShadeLds& 
 }
 
 // The heavy pixels' kernel (heavy pixels), launched after the pixel proof pass on
-// the context's side stream -- a queue of its own -- beside the batch kernel, which leaves room
-// for its blocks (rrt_host.cpp): each wave takes heavy pixels one at a time, at issue priority 3.
-template <int LEAN, int HW>
-__global__ __launch_bounds__(256, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp) {
+// the context's high-priority side stream, beside the batch kernel, which leaves room for its
+// blocks (rrt_host.cpp): each block of NW waves takes heavy pixels one at a time, at issue
+// priority 3.
+template <int LEAN, int HW, int NW>
+__global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
-  __shared__ ShadeLds cl;
-  const uint32_t t = threadIdx.x, lane = t & 63u;
+  __shared__ HeavyLds<NW> hl;
+  const uint32_t t = threadIdx.x;
   Counters cn = {};
   const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
   __builtin_amdgcn_s_setprio(3);
   for (;;) {
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(kp.heavy_count + 1, 1u);
-    k = __shfl(k, 0);
+    if (t == 0) hl.hx = atomicAdd(kp.heavy_count + 1, 1u);
+    __syncthreads();
+    const uint32_t k = hl.hx;
+    __syncthreads();  // every thread has read it before thread 0 claims again
     if (k >= nh) break;
 #if RRT_PROFILE
     const uint64_t w_h = wall_clock64();
 #endif
-    heavy_pixel_wave<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW)>(kp, cl, t, lane, k, cn);
+    heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl, t, k, cn);
 #if RRT_PROFILE  // elapsed ticks; "rounds" 1
-    if (lane == 0) {
+    if (t == 0) {
       const uint32_t ts = kp.tile_size, tpix = ts * ts;
       const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + ix % tpix;
       if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
@@ -496,17 +509,17 @@ __global__ __launch_bounds__(256, HW) void rrt_heavy_kernel(const KParams* __res
   }
 }
 
-hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream) {
-#define RRT_LAUNCH_H(L, W) hipLaunchKernelGGL((rrt_heavy_kernel<L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
+// waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream) {
+#define RRT_LAUNCH_H(L, W, N) hipLaunchKernelGGL((rrt_heavy_kernel<L, W, N>), dim3(grid), dim3(64 * N), 0, stream, d_kp)
   if (lean == 1) {
-    switch (waves) {
-      case 2: RRT_LAUNCH_H(1, 2); break;
-      case 3: RRT_LAUNCH_H(1, 3); break;
-      case 5: RRT_LAUNCH_H(1, 5); break;
-      default: RRT_LAUNCH_H(1, 4); break;
+    if (waves == 5) {
+      if (nw == 1) RRT_LAUNCH_H(1, 5, 1); else if (nw == 4) RRT_LAUNCH_H(1, 5, 4); else RRT_LAUNCH_H(1, 5, 2);
+    } else {
+      if (nw == 1) RRT_LAUNCH_H(1, 4, 1); else if (nw == 4) RRT_LAUNCH_H(1, 4, 4); else RRT_LAUNCH_H(1, 4, 2);
     }
   } else if (lean == 2) {
-    RRT_LAUNCH_H(2, 4);
+    RRT_LAUNCH_H(2, 4, 2);
   } else {
     return hipErrorInvalidValue;
   }

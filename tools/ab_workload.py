@@ -24,10 +24,11 @@ def main():
     ap.add_argument("--workload", default="cfg5", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--tile", type=int, default=32, help="tile size of the split (bench.py: 32)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
-    W, H, ts = wl["w"], wl["h"], 32
+    W, H, ts = wl["w"], wl["h"], a.tile
     work = tempfile.mkdtemp(prefix="rrt_ab_")
     r = rrt.Renderer(0)
     scene, cam, _, _ = bench.load_workload_scene(wl, work)
