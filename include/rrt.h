@@ -212,10 +212,10 @@ enum {
   RRT_RENDER_NO_HEAVY = 1u << 20, /* sample-parallel kernel: no slot-parallel path for heavy
                                      pixels (those whose rays straddle the hole's capture boundary
                                      or pass close to it; A/B and parity, results are identical) */
-  RRT_RENDER_HEAVY = 1u << 21,    /* sample-parallel kernel: the heavy pixels' path also for a
-                                     launch covering most of the frame (by default it runs only
-                                     for launches of at most 60% of the frame's pixels, e.g. one
-                                     rank's tiles of a multi-GPU frame; results are identical) */
+  RRT_RENDER_HEAVY = 1u << 21,    /* sample-parallel kernel: the heavy pixels' path for every
+                                     launch (by default it runs for launches of at most 60% of the
+                                     frame's pixels, e.g. one rank's tiles of a multi-GPU frame,
+                                     and when ns_aa >= 4 samples_per_batch; results are identical) */
   RRT_RENDER_DEEP_SAMPLE = 1u << 19, /* depth >= 2 (Schwarzschild): the per-sample refill kernel
                                      instead of the per-pixel loop (A/B; results are identical) */
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes

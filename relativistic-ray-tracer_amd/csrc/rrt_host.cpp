@@ -1402,12 +1402,15 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       // Heavy pixels (rrt_device.h pixel_heavy): the pass lists them apart and rrt_heavy_kernel
       // renders them slot-parallel, a block of waves per pixel (rrt_sample.hip
       // heavy_pixel_block); needs a hit to take a whole number of slots (Dh = k Dm)
-      // Only for launches covering at most 60% of the frame (one rank's tiles of a multi-GPU
-      // frame, the regions of the host path): there the heavy pixels' latency bounds the launch
-      // (cfg3 split 8 ways, slowest rank 7.6 -> 5.5 ms); a whole frame is bound by its throughput,
-      // and the heavy kernel's room in the batch grid costs more than it saves (18.2 -> 19.2 ms)
+      // Where the heavy pixels' latency bounds the launch: launches covering at most 60% of the
+      // frame (one rank's tiles of a multi-GPU frame, the regions of the host path; cfg3 split 8
+      // ways, slowest rank 8.1 -> 4.4 ms), and pixels of 4 or more adaptive steps, whose chains of
+      // rounds outlast the frame (cfg4, 256 spp: 16.5 -> 15.0 ms).  A whole cfg3 frame (2 steps a
+      // pixel) is bound by its throughput, and the heavy kernel's room in the batch grid costs more
+      // than it saves (18.3 -> 19.0 ms).
       const uint64_t frame_px = (uint64_t)p->frame_w * p->frame_h;
-      const bool share_ok = (p->flags & RRT_RENDER_HEAVY) || (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
+      const bool share_ok = (p->flags & RRT_RENDER_HEAVY) || (uint64_t)kp.n_pixels * 5u <= frame_px * 3u ||
+                            p->ns_aa >= 4u * p->samples_per_batch;
       if (!(p->flags & RRT_RENDER_NO_HEAVY) && share_ok && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0) {
         // at most 1/256 of the pixels (4096 at least): a frame mostly near the hole stays with
         // the batch kernel, whose rounds cost less than 64 slots a step for unmixed pixels
@@ -1481,7 +1484,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
     // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
     const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
-    const int w = lean == 1 ? bw : lean == 2 ? (bw >= 3 && bw <= 6 ? bw : 5) : gw;
+    const int w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 4) : gw;  // point-light build: 4 (cfg4 17.4 -> 17.0 ms)
     char first[32] = "";
     const uint32_t fwv = (p->variant >> 8) & 0xfu;  // pre-pass waves/SIMD (A/B), default 3
     const int fw = (lean == 1 && (fwv == 4 || fwv == 5)) ? (int)fwv : 3;
@@ -1501,7 +1504,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       // whichever kernel the hardware dispatches first
       const uint32_t hwv = (p->variant >> 24) & 0xfu, hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
       const int hw = hwv == 5 ? 5 : 4;
-      const int nw = (lean == 2 || nwv == 0) ? 2 : nwv == 1 ? 1 : 4;  // waves per heavy pixel
+      const int nw = nwv == 0 ? 2 : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;  // waves per heavy pixel
       // heavy waves: hgv x the CU count (default 2), in blocks of nw waves
       const uint32_t hwaves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
       const uint32_t hgrid = std::max<uint32_t>(1u, hwaves / (uint32_t)nw);

@@ -519,7 +519,7 @@ hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, ui
       if (nw == 1) RRT_LAUNCH_H(1, 4, 1); else if (nw == 4) RRT_LAUNCH_H(1, 4, 4); else RRT_LAUNCH_H(1, 4, 2);
     }
   } else if (lean == 2) {
-    RRT_LAUNCH_H(2, 4, 2);
+    if (nw == 4) RRT_LAUNCH_H(2, 4, 4); else RRT_LAUNCH_H(2, 4, 2);
   } else {
     return hipErrorInvalidValue;
   }

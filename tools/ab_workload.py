@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--tile", type=int, default=32, help="tile size of the split (bench.py: 32)")
+    ap.add_argument("--split", default="lib", help="lib (rrt_partition_tiles) or latS: rank = (tx + S ty) % world")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
@@ -37,7 +38,13 @@ def main():
     r.set_envmap(bench.load_workload_env(wl, work))
     kerr = wl.get("kerr")
     r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
-    sets = [rrt.partition_tiles(W, H, ts, k, a.world) for k in range(a.world)]
+    if a.split == "lib":
+        sets = [rrt.partition_tiles(W, H, ts, k, a.world) for k in range(a.world)]
+    else:  # A/B of other splits: a 2-D lattice of tiles over the ranks
+        sm = int(a.split[3:])
+        tw, th = (W + ts - 1) // ts, (H + ts - 1) // ts
+        sets = [np.array([(tx * ts, ty * ts) for ty in range(th) for tx in range(tw) if (tx + sm * ty) % a.world == k],
+                         np.uint32).reshape(-1, 2) for k in range(a.world)]
     n = max(len(t) for t in sets) * ts * ts
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
