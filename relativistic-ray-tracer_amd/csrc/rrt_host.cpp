@@ -1399,6 +1399,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       }
       kp.claim_list = c->d_list;
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
+      // hit-first claim order (rrt_pixel_proof_kernel); variant bit 22: the pass's order (A/B)
+      kp.claim_back = ((p->variant >> 22) & 1u) ? 0u : 1u;
       // Heavy pixels (rrt_device.h pixel_heavy): the pass lists them apart and rrt_heavy_kernel
       // renders them slot-parallel, a block of waves per pixel (rrt_sample.hip
       // heavy_pixel_block); needs a hit to take a whole number of slots (Dh = k Dm)

@@ -200,6 +200,7 @@ struct KParams {
   uint32_t* heavy_list;   // claim indices (null: no heavy path)
   uint32_t* heavy_count;  // [0]: entries appended by the pass (capped at heavy_cap); [1]: entries taken
   uint32_t heavy_cap;     // list capacity
-  uint32_t heavy_pad;
+  uint32_t claim_back;    // batch kernel: hinted list entries at the front (claim_count[0] of them),
+                          // the others from the list's end backwards (claim_count[1])
   double heavy_r2;        // (RRT_HEAVY_NEAR x r_s)^2: rays passing this close make a pixel heavy
 };

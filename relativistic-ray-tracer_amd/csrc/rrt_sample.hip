@@ -570,7 +570,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     if (needers) {
       // claim space: every pixel slot, or the pixel proof's list padded to whole stripes (the
       // padding claims no pixel); read here, not held through the kernel
-      const uint32_t n_list = kp.claim_list ? *kp.claim_count : 0u;
+      const uint32_t n_list = kp.claim_list ? *kp.claim_count + (kp.claim_back ? kp.claim_count[1] : 0u) : 0u;
       const uint32_t npx = kp.claim_list ? (n_list + STRIPE - 1) / STRIPE * STRIPE : kp.n_pixels;
       uint64_t pending = needers;
       uint32_t p = npx + 1;  // npx + 1: this group did not claim
@@ -622,7 +622,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         ++prof_blocks;
 #endif
         // a list entry: pixel claim index | hint << 31 (rrt_pixel_proof_kernel)
-        const uint32_t ent = kp.claim_list ? (p < n_list ? kp.claim_list[p] : kp.n_pixels) : p;
+        // (claim_back: the front part's entries, then the back part's from the list's end)
+        const uint32_t n_front = kp.claim_list ? *kp.claim_count : 0u;
+        const uint32_t ent = !kp.claim_list ? p
+                             : p < n_front ? kp.claim_list[p]
+                             : p < n_list ? kp.claim_list[kp.claim_back ? kp.n_pixels - 1u - (p - n_front) : p]
+                             : kp.n_pixels;
         const uint32_t ix = kp.claim_list ? (ent & 0x7fffffffu) : ent;
         const uint32_t pi = ix < kp.n_pixels ? ix : 0u;
         const uint32_t tl = kp.tile_order[pi / tpix], r = pi % tpix, lx = r % ts, ly = r / ts;
@@ -978,11 +983,26 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
     Counters cn = {};
     hint = camera_miss_proof<false>(kp, ld3(kp.cam.pos), pixel_ray_dir(kp, x + 0.5, y + 0.5), cn) ? 0u : 1u;
   }
-  const uint64_t b = __ballot(listed);
+  const uint64_t b = __ballot(listed), lt = (1ull << lane) - 1ull;
+  if (kp.claim_back) {
+    // hit-first claim order: hinted pixels (their central ray reaches the scene: shading and
+    // shadow rays, the costliest) from the list's front, the others from its back, so the
+    // cheap ones are claimed last and the launch ends on short pixels
+    const uint64_t bf = __ballot(listed && hint), bb = b & ~bf;
+    uint32_t basef = 0, baseb = 0;
+    if (lane == 0) {
+      if (bf) basef = atomicAdd(kp.claim_count, (uint32_t)__popcll(bf));
+      if (bb) baseb = atomicAdd(kp.claim_count + 1, (uint32_t)__popcll(bb));
+    }
+    basef = __shfl(basef, 0); baseb = __shfl(baseb, 0);
+    if (listed && hint) kp.claim_list[basef + (uint32_t)__popcll(bf & lt)] = ix | (1u << 31);
+    else if (listed) kp.claim_list[kp.n_pixels - 1u - (baseb + (uint32_t)__popcll(bb & lt))] = ix;
+    return;
+  }
   uint32_t base = 0;
   if (lane == 0 && b) base = atomicAdd(kp.claim_count, (uint32_t)__popcll(b));
   base = __shfl(base, 0);
-  if (listed) kp.claim_list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = ix | (hint << 31);
+  if (listed) kp.claim_list[base + (uint32_t)__popcll(b & lt)] = ix | (hint << 31);
 }
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream) {
   hipLaunchKernelGGL(rrt_pixel_proof_kernel, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_kp);
