@@ -96,7 +96,7 @@ for step in "$@"; do
     abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 2 0 2 4 0:16 0:131072 ;;
     deeptests) run pytest_deep 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
     pmcall) # PMC of every workload's main kernel on this build, copied into profiles/ for the bench lines
-           for wk in "cfg3:rrt_batch_kernel<1, 5>" "cfg4:rrt_batch_kernel<2, 5>" "cfg5:rrt_batch_kernel<3, 3>" "cfg2:rrt_batch_kernel<1, 5>"; do
+           for wk in "cfg3:rrt_batch_kernel<1, 5>" "cfg4:rrt_batch_kernel<2, 4>" "cfg2:rrt_batch_kernel<1, 5>" "m3:rrt_render_kernel<true, false, 0, ...>" "cfg5:rrt_batch_kernel<3, 3>"; do
              PMC_WORKLOAD=${wk%%:*} PMC_KERNEL=${wk#*:} bash tools/gpu_session.sh valu || exit $?
              cp gpurun_out/r03_${wk%%:*}_pmc.json profiles/ ; done ;;
     profall) run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&

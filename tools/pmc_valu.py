@@ -18,7 +18,10 @@ import os
 
 
 def per_dispatch(dirs, match):
-    """{counter: mean over dispatches of the kernels whose name contains `match`} + durations."""
+    """{counter: mean over dispatches of the kernels whose name contains `match`} + durations.
+    A name librrt abbreviates ("rrt_render_kernel<true, false, 0, ...>") matches by its prefix."""
+    if match.endswith("...>"):
+        match = match[:-4]
     vals, durs = {}, {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
