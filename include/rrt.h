@@ -249,7 +249,10 @@ int rrt_render(rrt_ctx* ctx, const rrt_render_params* p, uint32_t x0, uint32_t y
  * tiles is a host array of 2*n_tiles uint32.  A context owns one launch workspace (parameters,
  * claim counters, tile list): a launch or unpack on a different stream than the context's
  * previous one makes its stream wait for that previous use first (hipStreamWaitEvent), so
- * launches of one context never overlap; use one context per stream to overlap renders. */
+ * launches of one context never overlap; use one context per stream to overlap renders.
+ * The heavy pixels' kernel (RRT_RENDER_HEAVY) runs on the context's own high-priority side
+ * stream, forked from `stream` after the pixel proof pass and joined back into it (events)
+ * before the launch ends: work the caller enqueues on `stream` afterwards sees the whole frame. */
 int rrt_render_tiles_device(rrt_ctx* ctx, const rrt_render_params* p, const uint32_t* tiles, uint32_t n_tiles,
                             uint32_t tile_size, float* d_rgb, int32_t* d_count, uint32_t* d_counters,
                             void* stream);
