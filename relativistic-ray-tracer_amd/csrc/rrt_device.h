@@ -404,6 +404,7 @@ __device__ __forceinline__ bool traverse_free(const KParams& kp, v3 o, v3 d, v3 
                                               uint64_t bmask = ~0ull) {
   if (COUNT) cn.bbox++;
   if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return false;
+  bmask &= kp.free_big_mask;  // the local oversized leaves sit in the search tree
   const double L = max_t;
   const v3 e = o + vmul(d, L);
   const int nb = (int)kp.n_big;

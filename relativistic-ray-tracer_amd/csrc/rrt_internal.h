@@ -203,4 +203,6 @@ struct KParams {
   uint32_t claim_back;    // batch kernel: hinted list entries at the front (claim_count[0] of them),
                           // the others from the list's end backwards (claim_count[1])
   double heavy_r2;        // (RRT_HEAVY_NEAR x r_s)^2: rays passing this close make a pixel heavy
+  uint64_t free_big_mask; // oversized leaves traverse_free tests from its list (the others are in
+                          // the search tree); ~0 for the clean-tree and reference-tree walks
 };

@@ -333,7 +333,15 @@ def test_search_walk_matches_reference_walk(host_ctx, scene):
     cb, cn = ct[0], ct[1]
     leaves_clean = sorted((int(r[1]), int(r[2]), tuple(cb[i])) for i, r in enumerate(cn) if r[2] > 0)
     leaves_search = sorted((int(r[1]), int(r[2]), tuple(sb[i])) for i, r in enumerate(sn) if r[2] > 0)
-    assert leaves_clean == leaves_search
+    # the search tree holds the clean tree's leaves plus the local oversized ones (box diagonal at
+    # most a quarter of the root's); the room-spanning ones stay on the walk's list
+    bb, bg = ct[2], ct[3]
+    root = host_ctx.bvh()[0][0]
+    rd = float(np.linalg.norm(root[3:] - root[:3]))
+    local = sorted((int(bg[i, 0]), int(bg[i, 1]), tuple(bb[i])) for i in range(len(bg))
+                   if np.linalg.norm(bb[i, 3:] - bb[i, :3]) <= 0.25 * rd)
+    assert leaves_search == sorted(leaves_clean + local)
+    assert len(local) < len(bg)
     # pre-order with skip pointers; every inner box contains its subtree
     n = len(sn)
     end = [0] * n

@@ -77,6 +77,11 @@ class Walker:
         boxes, nodes = st
         self.sboxes = [tuple(b) for b in boxes]
         self.snodes = [tuple(int(v) for v in r) for r in nodes]
+        # the oversized leaves that joined the search tree (rrt_host.cpp build_free_tree: the local
+        # ones) leave the walk's list
+        inside = {(f, c) for _, f, c, _ in self.snodes if c > 0}
+        self.big_all = self.big
+        self.big = [b for b in self.big if (b[1], b[2]) not in inside]
 
     def _tri_or_sphere(self, s, o, d, max_t):
         g = self.geo[s]
