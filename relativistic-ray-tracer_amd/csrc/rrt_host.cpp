@@ -1503,11 +1503,13 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const char* tf[2] = {"false", "true"};
   char name[96];
   if (batch) {
-    // 5 waves/SIMD measured best on cfg3 (spills are cheap; latency hiding is not)
-    const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 5;
+    // waves/SIMD: the area-light build at 4 (cfg3 15.71 -> 15.33 ms, cfg2 10.33 -> 10.01 ms against
+    // 5, since the search tree took the local oversized leaves), the point-light build at 5 (cfg4
+    // 14.15 ms against 14.65 at 4) -- profiles/r03_heavy_ab.md
+    const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 4;
     // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
     const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
-    const int w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 4) : gw;  // point-light build: 4 (cfg4 17.4 -> 17.0 ms)
+    const int w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 5) : gw;
     char first[32] = "";
     const uint32_t fwv = (p->variant >> 8) & 0xfu;  // pre-pass waves/SIMD (A/B), default 3
     const int fw = (lean == 1 && (fwv == 4 || fwv == 5)) ? (int)fwv : 3;

@@ -64,7 +64,7 @@ for step in "$@"; do
            run crop_tiles 300 python3 tools/crop_probe.py --region 960 576 32 64 --no-counters --flags 0 ;;
     valu)  # PMC passes over the bench's launches (-> tools/pmc_valu.py): FP64 VALU mix, lane utilisation,
            # clock; HBM fetch / write.  One rocprofv3 run per pass.
-           W=${PMC_WORKLOAD:-cfg3}; K=${PMC_KERNEL:-rrt_batch_kernel<1, 5>}
+           W=${PMC_WORKLOAD:-cfg3}; K=${PMC_KERNEL:-rrt_batch_kernel<1, 4>}
            run pmc_valu_$W 600 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmcv_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
            run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmcf_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
            run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmcw_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
@@ -96,7 +96,7 @@ for step in "$@"; do
     abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 2 0 2 4 0:16 0:131072 ;;
     deeptests) run pytest_deep 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
     pmcall) # PMC of every workload's main kernel on this build, copied into profiles/ for the bench lines
-           for wk in "cfg3:rrt_batch_kernel<1, 5>" "cfg4:rrt_batch_kernel<2, 4>" "cfg2:rrt_batch_kernel<1, 5>" "m3:rrt_render_kernel<true, false, 0, ...>" "cfg5:rrt_batch_kernel<3, 3>"; do
+           for wk in "cfg3:rrt_batch_kernel<1, 4>" "cfg4:rrt_batch_kernel<2, 5>" "cfg2:rrt_batch_kernel<1, 4>" "m3:rrt_render_kernel<true, false, 0, ...>" "cfg5:rrt_batch_kernel<3, 3>"; do
              PMC_WORKLOAD=${wk%%:*} PMC_KERNEL=${wk#*:} bash tools/gpu_session.sh valu || exit $?
              cp gpurun_out/r03_${wk%%:*}_pmc.json profiles/ ; done ;;
     profall) run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
