@@ -26,7 +26,11 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 2  /* 2: rrt_spacetime_desc gained spin + axis (Kerr) */
+#define RRT_ABI_VERSION 3  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
+                              3: rrt_stats gained last_main_kernel_ms / last_heavy_pixels (callers
+                                 built against 2 pass a smaller struct: rebuild), the
+                                 RRT_RENDER_WAVEFRONT flag is rejected (RRT_E_INVALID),
+                                 rrt_libm_eval added */
 
 enum {
   RRT_OK = 0,
@@ -298,6 +302,12 @@ typedef struct {
   uint32_t last_heavy_pixels;  /* pixels the last launch rendered slot-parallel (heavy pixels) */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
+/* Diagnostics: evaluate the device's restatement of the host C library's transcendentals
+ * (csrc/rrt_glibm.h -- the reference's sin/cos (sampler.cpp:53-55, environment_light.cpp:97-137),
+ * acos (sampler.cpp:20, bsdf.h:166, environment_light.cpp:88), atan2 (environment_light.cpp:89),
+ * sinf/cosf (sampler.cpp:23-25)) on n host arguments: fn 0 sin(a), 1 cos(a), 2 acos(a),
+ * 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a) (float results widened to double). */
+int rrt_libm_eval(rrt_ctx* ctx, int fn, const double* a, const double* b, double* out, uint64_t n);
 /* HIP-event times of the last n (<= 32) render launches, oldest first: the whole launch and its
  * main kernel alone (bench.py's roofline divides by the latter).  Returns the count filled. */
 int rrt_get_launch_times(const rrt_ctx* ctx, uint32_t n, float* total_ms, float* main_ms);

@@ -1203,3 +1203,20 @@ void ro_camera_ray(double hFov, double vFov, const double* pos, const double* c2
   o[0] = oo.x; o[1] = oo.y; o[2] = oo.z; d[0] = dd.x; d[1] = dd.y; d[2] = dd.z;
   *min_t = nClip; *max_t = fClip;
 }
+
+/* ------------------------------------------------------------------ the host C library itself */
+/* The reference's transcendentals as the reference gets them: straight from this machine's libm
+ * (glibc).  tests/test_gpu_glibm.py compares the device restatement (rrt_libm_eval) with these.
+ * fn: 0 sin, 1 cos, 2 acos, 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a). */
+void ro_libm_eval(int fn, const double* a, const double* b, double* out, long n) {
+  for (long k = 0; k < n; ++k) {
+    switch (fn) {
+      case 0: out[k] = sin(a[k]); break;
+      case 1: out[k] = cos(a[k]); break;
+      case 2: out[k] = acos(a[k]); break;
+      case 3: out[k] = atan2(a[k], b[k]); break;
+      case 4: out[k] = sinf((float)a[k]); break;
+      default: out[k] = cosf((float)a[k]); break;
+    }
+  }
+}

@@ -98,4 +98,7 @@ void ro_camera_ray(double hFov, double vFov, const double* pos, const double* c2
 #ifdef __cplusplus
 }
 #endif
+/* the host C library's sin/cos/acos/atan2/sinf/cosf on n arguments (checker for rrt_libm_eval) */
+void ro_libm_eval(int fn, const double* a, const double* b, double* out, long n);
+
 #endif

@@ -5,8 +5,9 @@
 // the reference's narrowing points, the same operation order, no FMA contraction (the pragma
 // below plus -ffp-contract=off), IEEE division / sqrt.  Transcendentals whose arguments are
 // per-run constants (tan of the half FOV, cos/sin of delta_theta) come from the host libm, i.e.
-// the values the reference uses; per-sample transcendentals (bounce / hemisphere / microfacet
-// paths only) use the device libm.
+// the values the reference uses; per-sample sin, cos, acos, atan2, sinf and cosf are the host C
+// library's own routines restated in rrt_glibm.h (bit-identical); the microfacet BSDF's tan, exp,
+// log, atan and erf still use the device libm.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -14,6 +15,7 @@
 
 #include "rrt_internal.h"
 #include "rrt_rng.h"
+#include "rrt_glibm.h"
 
 #pragma clang fp contract(off)
 
@@ -115,16 +117,16 @@ __device__ __forceinline__ v3 cosine_sample(Rng& g, float* pdf) {  // sampler.cp
   double r = sqrt(Xi1);
   double theta = 2. * PI_D * Xi2;
   *pdf = (float)(sqrt(1 - Xi1) / PI_D);
-  return V(r * cos(theta), r * sin(theta), sqrt(1 - Xi1));
+  return V(r * rrt_glibm_cos(theta), r * rrt_glibm_sin(theta), sqrt(1 - Xi1));
 }
 __device__ __forceinline__ v3 hemisphere_sample(Rng& g) {  // sampler.cpp:15-29 (float trig)
   double Xi1 = g.uniform();
   double Xi2 = g.uniform();
-  double theta = acos(Xi1);
+  double theta = rrt_glibm_acos(Xi1);
   double phi = 2.0 * PI_D * Xi2;
-  double xs = sinf((float)theta) * cosf((float)phi);
-  double ys = sinf((float)theta) * sinf((float)phi);
-  double zs = cosf((float)theta);
+  double xs = rrt_glibm_sinf((float)theta) * rrt_glibm_cosf((float)phi);
+  double ys = rrt_glibm_sinf((float)theta) * rrt_glibm_sinf((float)phi);
+  double zs = rrt_glibm_cosf((float)theta);
   return V(xs, ys, zs);
 }
 
@@ -1339,7 +1341,7 @@ __device__ __forceinline__ spec emission(const DBsdf& b) {
   return b.type == B_EMISSION ? S(b.p[0], b.p[1], b.p[2]) : S(0, 0, 0);
 }
 __device__ __forceinline__ double clamp_b(double n, double lo, double hi) { return std_max(lo, std_min(n, hi)); }
-__device__ __forceinline__ double mf_theta(v3 w) { return acos(clamp_b(w.z, -1.0 + 1e-5, 1.0 - 1e-5)); }
+__device__ __forceinline__ double mf_theta(v3 w) { return rrt_glibm_acos(clamp_b(w.z, -1.0 + 1e-5, 1.0 - 1e-5)); }
 __device__ __forceinline__ double mf_lambda(float alpha, v3 w) {
   double theta = mf_theta(w);
   double a = 1.0 / (alpha * tan(theta));
@@ -1416,10 +1418,10 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf)
       double alpha2 = alpha * alpha,
              theta_h = atan(sqrt(-alpha2 * log(1 - ux))),
              phi_h = 2 * PI_D * uy,
-             sin_h = sin(theta_h), cos_h = cos(theta_h), tan_h = tan(theta_h),
+             sin_h = rrt_glibm_sin(theta_h), cos_h = rrt_glibm_cos(theta_h), tan_h = tan(theta_h),
              p_theta = 2 * sin_h * exp(-tan_h * tan_h / alpha2) / (alpha2 * cos_h * cos_h * cos_h),
              p_phi = 0.5 / PI_D;
-      v3 h = V(sin_h * cos(phi_h), sin_h * sin(phi_h), cos_h);
+      v3 h = V(sin_h * rrt_glibm_cos(phi_h), sin_h * rrt_glibm_sin(phi_h), cos_h);
       wi = smul(2 * dot(wo, h), h) - wo;
       if (wi.z <= 0) { pdf = 0; return S(0, 0, 0); }
       pdf = (float)(p_theta * p_phi / (sin_h * 4 * dot(wi, h)));
@@ -1456,9 +1458,9 @@ __device__ spec env_bilerp(const DEnv& e, double xx, double yy) {  // :112-127
          ((env_texel(e, bottom + left) * fu1) + (env_texel(e, bottom + right) * fu0)) * fv0;
 }
 // sample_dir (:146-148): radiance seen along direction d (the unbent camera ray on a miss)
-__device__ spec env_dir(const DEnv& e, v3 d) {
+__device__ __forceinline__ spec env_dir(const DEnv& e, v3 d) {
   const v3 u = unit(d);
-  const double theta = acos(u.y), phi = atan2(-u.z, u.x) + PI_D;  // dir_to_theta_phi (:89-94)
+  const double theta = rrt_glibm_acos(u.y), phi = rrt_glibm_atan2(-u.z, u.x) + PI_D;  // dir_to_theta_phi (:89-94)
   const double x = phi / 2. / PI_D * e.w, y = theta / PI_D * e.h;  // theta_phi_to_xy (:71-77)
   return env_bilerp(e, x, y);
 }
@@ -1473,7 +1475,7 @@ __device__ __forceinline__ uint32_t upper_bound_d(const double* a, uint32_t n, d
   return first;
 }
 // sample_L (:130-144, ENV_HEMI == 0): row by the marginal CDF, column by the row's conditional CDF
-__device__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float& dist, float& pdf) {
+__device__ __forceinline__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float& dist, float& pdf) {
   dist = INFINITY;
   double sx, sy;
   g.grid(sx, sy);
@@ -1482,8 +1484,9 @@ __device__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float& dist, float& pd
   uint32_t x = upper_bound_d(e.conds + (size_t)e.w * y, e.w, sx);
   if (x >= e.w) x = e.w - 1;
   const double phi = (double)x / e.w * 2.0 * PI_D, theta = (double)y / e.h * PI_D;  // xy_to_theta_phi
-  wi = V(cos(phi - PI_D) * sin(theta), cos(theta), -sin(phi - PI_D) * sin(theta));  // theta_phi_to_dir
-  pdf = (float)(e.pdf[(size_t)e.w * y + x] * e.w * e.h / (2 * PI_D * PI_D * sin(theta)));
+  wi = V(rrt_glibm_cos(phi - PI_D) * rrt_glibm_sin(theta), rrt_glibm_cos(theta),
+         -rrt_glibm_sin(phi - PI_D) * rrt_glibm_sin(theta));  // theta_phi_to_dir
+  pdf = (float)(e.pdf[(size_t)e.w * y + x] * e.w * e.h / (2 * PI_D * PI_D * rrt_glibm_sin(theta)));
   return env_bilerp(e, (double)x, (double)y);
 }
 

@@ -30,6 +30,7 @@ hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStr
 hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
+hipError_t rrt_launch_libm(int fn, uint64_t n, const double* a, const double* b, double* out, hipStream_t stream);
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,
                               hipStream_t stream);
 
@@ -1602,6 +1603,29 @@ extern "C" int rrt_tonemap_device(rrt_ctx* c, uint32_t n, const float* rgb, uint
   const float inv_gamma = 1.0f / 2.2f;
   const float exposure = (float)std::sqrt(std::pow(2, 1.0f));
   HIPCHK(c, rrt_launch_tonemap(n, rgb, rgba, exposure, inv_gamma, s));
+  return RRT_OK;
+}
+
+extern "C" int rrt_libm_eval(rrt_ctx* c, int fn, const double* a, const double* b, double* out, uint64_t n) {
+  if (!c || !a || !out || fn < 0 || fn > 5 || (fn == 3 && !b)) return fail(c, RRT_E_INVALID, "bad argument");
+  if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "no device");
+  if (n == 0) return RRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  double *da = nullptr, *db = nullptr, *dout = nullptr;
+  struct Free {
+    double** p[3];
+    ~Free() { for (double** q : p) if (*q) (void)hipFree(*q); }
+  } guard{{&da, &db, &dout}};
+  const size_t bytes = sizeof(double) * n;
+  HIPCHK(c, hipMalloc(&da, bytes));
+  HIPCHK(c, hipMalloc(&dout, bytes));
+  HIPCHK(c, hipMemcpy(da, a, bytes, hipMemcpyHostToDevice));
+  if (fn == 3) {
+    HIPCHK(c, hipMalloc(&db, bytes));
+    HIPCHK(c, hipMemcpy(db, b, bytes, hipMemcpyHostToDevice));
+  }
+  HIPCHK(c, rrt_launch_libm(fn, n, da, db, dout, (hipStream_t)0));
+  HIPCHK(c, hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
   return RRT_OK;
 }
 

@@ -139,6 +139,25 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
   }
 }
 
+// The device's restatements of the host C library's functions (rrt_glibm.h), evaluated on n
+// arguments: rrt_libm_eval checks them bit for bit against the host's libm (tests/test_gpu_glibm.py).
+// fn: 0 sin, 1 cos, 2 acos, 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a)
+__global__ void rrt_libm_kernel(int fn, uint64_t n, const double* a, const double* b, double* out) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const double x = a[k];
+    double r;
+    switch (fn) {
+      case 0: r = rrt_glibm_sin(x); break;
+      case 1: r = rrt_glibm_cos(x); break;
+      case 2: r = rrt_glibm_acos(x); break;
+      case 3: r = rrt_glibm_atan2(x, b[k]); break;
+      case 4: r = rrt_glibm_sinf((float)x); break;
+      default: r = rrt_glibm_cosf((float)x); break;
+    }
+    out[k] = r;
+  }
+}
+
 // ------------------------------------------------------------------ launch shims (C++ linkage)
 // Kernel selection: deep / counting variants are built once (1 wave per SIMD budget); the
 // depth <= 1 path has general and LEAN builds at 1..4 waves per SIMD (A/B knob `waves`).
@@ -189,6 +208,13 @@ hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t t
   if (grid == 0) grid = 1;
   hipLaunchKernelGGL(rrt_unpack_kernel, dim3(grid), dim3(256), 0, stream, tiles, n_tiles, ts, fw, fh, rgb_p, cnt_p,
                      rgb, cnt);
+  return hipGetLastError();
+}
+hipError_t rrt_launch_libm(int fn, uint64_t n, const double* a, const double* b, double* out, hipStream_t stream) {
+  uint64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(rrt_libm_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, fn, n, a, b, out);
   return hipGetLastError();
 }
 hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float exposure, float inv_gamma,

@@ -100,7 +100,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
            "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
-           "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy"]
+           "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy", "rrt_libm_eval"]
 
 _lib = None
 
@@ -146,6 +146,7 @@ def lib():
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_launch_times.argtypes = [vp, C.c_uint32, vp, vp]
+        L.rrt_libm_eval.argtypes = [vp, C.c_int, vp, vp, vp, C.c_uint64]
         L.rrt_proof_envelope.argtypes = [vp]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
         for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_search_tree", 3),
@@ -379,6 +380,16 @@ class Renderer:
         d = EnvmapDesc()
         d.width, d.height, d.texels = t.shape[1], t.shape[0], t.ctypes.data
         self._chk(lib().rrt_set_envmap(self.h, C.byref(d)))
+
+    LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5}
+
+    def libm_eval(self, fn, a, b=None):
+        """The device's restated host-libm function `fn` (rrt_glibm.h) on float64 arrays a (, b)."""
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+        out = np.empty_like(a)
+        self._chk(lib().rrt_libm_eval(self.h, self.LIBM_FN[fn], _p(a), _p(b), _p(out), a.size))
+        return out
 
     def render(self, params, x0, y0, w, h, draws=False, counters=False):
         rgb = np.zeros((h, w, 3), np.float32)

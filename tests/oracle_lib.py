@@ -74,6 +74,7 @@ def lib():
         L.ro_camera_ray.argtypes = [C.c_double, C.c_double, _f64p, _f64p, C.c_double, C.c_double, C.c_double,
                                     C.c_double, _f64p, _f64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.ro_scene_set_envmap.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+        L.ro_libm_eval.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long]
         _lib = L
     return _lib
 
@@ -152,3 +153,15 @@ def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):
     if rc != 0:
         raise RuntimeError("ro_render failed")
     return rgb, cnt, draws, ctr
+
+
+LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5}
+
+
+def libm_eval(fn, a, b=None):
+    """The host C library's `fn` (what the reference calls) on float64 arrays a (, b)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty_like(a)
+    lib().ro_libm_eval(LIBM_FN[fn], a.ctypes.data, None if b is None else b.ctypes.data, out.ctypes.data, a.size)
+    return out

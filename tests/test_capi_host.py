@@ -22,7 +22,7 @@ def test_exports_match_header():
     L = rrt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rrt_abi_version() == 2
+    assert L.rrt_abi_version() == 3
 
 
 @pytest.fixture(scope="module")

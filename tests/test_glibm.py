@@ -1,0 +1,78 @@
+"""The device's restatement of the host C library's transcendentals (csrc/rrt_glibm.h) against the
+library itself, on the CPU: the same source compiled as C must return the library's bits.
+
+The reference calls glibc's sin/cos (sampler.cpp:53-55 cosine-weighted hemisphere sampler of every
+diffuse bounce; environment_light.cpp:97-137), acos (sampler.cpp:20, bsdf.h:166,
+environment_light.cpp:88), atan2 (environment_light.cpp:89) and sinf/cosf (sampler.cpp:23-25).
+Checked here (tests/glibm_check.c):
+  * every argument the samplers can produce: Xi = k / RAND_MAX for all 2^31 k, through
+    cos/sin(2 PI Xi), acos(Xi), (float)acos(Xi) and sinf/cosf of (float)acos(Xi), (float)(2 PI Xi);
+  * sinf and cosf on every float of the restated domain |x| < 120;
+  * 10^8 random arguments per function (value- and log-uniform; atan2 also on unit directions);
+  * every branch boundary, zeros, infinities and NaNs.
+The GPU side of the same check is tests/test_gpu_glibm.py.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "relativistic-ray-tracer_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    exe = str(tmp_path_factory.mktemp("glibm") / "glibm_check")
+    subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fopenmp", "-I", CSRC,
+                    os.path.join(ROOT, "tests", "glibm_check.c"), "-o", exe, "-lm"], check=True)
+    return exe
+
+
+def run(exe, *args):
+    r = subprocess.run([exe, *map(str, args)], capture_output=True, text=True, timeout=600)
+    res = json.loads(r.stdout)
+    print(res)
+    for name, v in res.items():
+        if name != "mode":
+            tested, bad, first = v
+            assert tested > 0 and bad == 0, f"{name}: {bad} of {tested} differ from the library (first at {first!r})"
+    assert r.returncode == 0
+    return res
+
+
+def test_tables_are_the_librarys():
+    """rrt_glibm_tables.h is what tools/gen_glibm_tables.py reads from this machine's libm."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen", os.path.join(ROOT, "tools", "gen_glibm_tables.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    import hashlib
+    data = open(gen.LIBM, "rb").read()
+    if hashlib.sha256(data).hexdigest() != gen.LIBM_SHA256:
+        pytest.skip("a different libm build: the restatement is pinned to " + gen.EXPECTED)
+    assert gen.render(data) == open(gen.OUT).read()
+
+
+def test_branch_boundaries_and_specials(checker):
+    run(checker, "specials")
+
+
+def test_random_arguments(checker):
+    res = run(checker, "random", 100_000_000, 20261017)
+    assert res["sin"][0] == 100_000_000 and res["atan2"][0] == 100_000_000
+
+
+def test_every_float_below_120(checker):
+    run(checker, "floats", 0, 0x42F00000)            # +0 .. 120
+    run(checker, "floats", 0x80000000, 0xC2F00000)   # -0 .. -120
+
+
+def test_every_sampler_argument(checker):
+    """All 2^31 values random_uniform() can return, through each reference call site."""
+    res = run(checker, "sampler", 0, 2 ** 31)
+    assert res["cos"][0] == 2 ** 31

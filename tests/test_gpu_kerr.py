@@ -2,10 +2,10 @@
 against the CPU restatement (oracle/restate ro_render with bh_kind = Kerr) on the same inputs.
 
 Parity against the reference is UNPINNED (the reference has no Kerr metric); the restatement is
-pinned by physics in tests/test_kerr_oracle.py.  The Kerr march uses only + - * / sqrt, so the
-same exactness rule as the reference cases applies: depth <= 1 with importance-sampled direct
-light is bit-exact (RGB, sample counts, RNG draws); bounce / hemisphere / environment-map paths
-(device libm transcendentals) meet the north-star tolerance RMS |dRGB|_2 <= 1e-4."""
+pinned by physics in tests/test_kerr_oracle.py.  The Kerr march uses only + - * / sqrt, and the
+per-sample sin/cos/acos/atan2/sinf/cosf are the host C library's own routines restated on the
+device (rrt_glibm.h), so the same exactness rule as the reference cases applies: every case
+without a microfacet BSDF is bit-exact (RGB, sample counts, RNG draws)."""
 import numpy as np
 import pytest
 
@@ -82,8 +82,8 @@ def test_kerr_matches_restatement(gpu, name, spin, axis, variant):
         assert np.array_equal(cnt, ref_cnt)
         assert np.array_equal(draws, ref_draws)
     else:
-        assert m["rms"] <= TOL and m["rms_nonblack"] <= TOL, m
-        assert np.mean(cnt == ref_cnt) > 0.99
+        assert m["max"] <= TOL, m  # north star: per-pixel L2 <= 1e-4 on every pixel
+        assert np.array_equal(cnt, ref_cnt)
 
 
 def test_kerr_differs_from_schwarzschild(gpu):

@@ -1,9 +1,10 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's golden outputs.
 
-Tolerance (north star): per-pixel L2 of linear HDR RGB, RMS over pixels <= 1e-4, and the same
-RMS over non-black pixels only.  Cases whose hot path uses no per-sample transcendental
-(Case.exact: depth <= 1, importance-sampled direct light) must be bit-exact, including the
-per-pixel sample counts and RNG draw counts."""
+Every case without a microfacet BSDF (Case.exact) must be bit-exact, including the per-pixel
+sample counts and RNG draw counts: the bounce, hemisphere and environment paths' sin/cos/acos/
+atan2/sinf/cosf are the host C library's own routines restated on the device (rrt_glibm.h).
+The microfacet cases (tan/exp/log/atan/erf from the device libm) are held to the north-star
+tolerance on every pixel: max over pixels of the per-pixel L2 of linear HDR RGB <= 1e-4."""
 import os
 
 import numpy as np
@@ -45,12 +46,9 @@ def check(c, rgb, cnt, draws):
         if draws is not None:
             assert np.array_equal(draws, c.px["draws"])
     else:
-        # north star: per-pixel L2 <= 1e-4.  A device-libm ulp in a transcendental can flip one
-        # sample's branch (a bounce, a coin flip) and move that pixel by more; such outliers stay
-        # rare (<= 1% of pixels) and the RMS over all and over lit pixels stays within tolerance
-        assert m["rms"] <= TOL and m["rms_nonblack"] <= TOL, m
-        assert m["over_tol_frac"] <= 0.01, m
-        assert np.mean(cnt == c.px["count"]) > 0.99
+        # north star: per-pixel L2 <= 1e-4, on every pixel
+        assert m["max"] <= TOL, m
+        assert np.array_equal(cnt, c.px["count"]), m
     return m
 
 
