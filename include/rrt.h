@@ -222,6 +222,21 @@ enum {
                                      and when ns_aa >= 4 samples_per_batch; results are identical) */
   RRT_RENDER_DEEP_SAMPLE = 1u << 19, /* depth >= 2 (Schwarzschild): the per-sample refill kernel
                                      instead of the per-pixel loop (A/B; results are identical) */
+  /* The reference's compile-time switches (pathtracer.h:4-6, environment_light.h:4, bsdf.h:4) as
+   * run-time flags; 0 is the reference build's setting.  Any of them selects the general
+   * per-pixel-loop kernel build that carries them (every ray marched exactly; Schwarzschild only;
+   * parity against the restatement: the reference's switches are #defines this harness cannot flip): */
+  RRT_RENDER_THIN_LENS = 1u << 22, /* THIN_LENS 1: Camera::generate_ray_for_thin_lens (camera.cpp:176-184)
+                                     with the camera's lensRadius / focalDistance; its lens sample comes
+                                     from the grid sampler after the pixel jitter (part1_code.cpp:137-139) */
+  RRT_RENDER_NO_ADAPTIVE = 1u << 23, /* ADAPTIVE 0: every pixel takes ns_aa samples (part1_code.cpp:147-159) */
+  RRT_RENDER_ENV_HEMI = 1u << 24, /* ENV_HEMI 1: EnvironmentLight::sample_L samples the uniform sphere
+                                     (environment_light.cpp:139-142, sampler.cpp:33-40) */
+  RRT_RENDER_MICROFACET_HEMI = 1u << 25, /* MICROFACET_HEMI 1: MicrofacetBSDF::sample_f takes the
+                                     cosine hemisphere sampler (bsdf.cpp:93-94) */
+  /* bits 26..27: ILLUM (pathtracer.h:4) xor 2, see RRT_RENDER_ILLUM: 0 normal shading,
+     1 direct lighting only, 2 the default, 3 at_least_one_bounce_radiance alone (part1_code.cpp:78-122) */
+  RRT_RENDER_ILLUM_MASK = 3u << 26,
   RRT_RENDER_COUNT_EXECUTED = 1u << 8, /* with COUNTERS: count the work the renderer executes
                                      (AABB tests incl. oversized leaves, primitive tests after
                                      the plane cull, micro steps, and plane tests in place of
@@ -233,6 +248,7 @@ enum {
   RRT_RENDER_DIAG_CLEAR_STATS = 1u << 31  /* with COUNTERS: counter 3 = grid-clear segments,
                                              counter 2 = AABB tests outside them */
 };
+#define RRT_RENDER_ILLUM(n) ((((uint32_t)(n)) ^ 2u) << 26)  /* ILLUM n as flag bits (ILLUM 2: 0) */
 void rrt_render_params_default(rrt_render_params* p);
 
 /* Replaces: PathTracer::raytrace_tile / raytrace_cell over the region [x0,x0+w) x [y0,y0+h)

@@ -333,6 +333,7 @@ void ro_params_default(ro_params* p) {
   p->ns_aa = 1; p->max_ray_depth = 1; p->ns_area_light = 1; p->samples_per_batch = 32;
   p->max_tolerance = 0.05f; p->direct_hemisphere = 0; p->seed = 0;
   p->bh_center[0] = 0; p->bh_center[1] = 1; p->bh_center[2] = 0; p->bh_radius = 0.1; p->bh_dtheta = 0.1;
+  p->illum = 2; p->adaptive = 1; p->thin_lens = 0; p->env_hemi = 0; p->microfacet_hemi = 0;  /* ILLUM, ADAPTIVE, ... */
 }
 
 /* ------------------------------------------------------------------ rays & geometry */
@@ -703,7 +704,11 @@ static inline int refract(v3 wo, v3* wi, float ior) { /* bsdf.cpp:146-159 */
   if (wo.z > 0) wi->z = -wi->z;
   return 1;
 }
+static spec bsdf_sample_f_sw(const bsdf_t* b, rng_t* g, v3 wo, v3* wi, float* pdf, int mf_hemi);
 static spec bsdf_sample_f(const bsdf_t* b, rng_t* g, v3 wo, v3* wi, float* pdf) {
+  return bsdf_sample_f_sw(b, g, wo, wi, pdf, 0);
+}
+static spec bsdf_sample_f_sw(const bsdf_t* b, rng_t* g, v3 wo, v3* wi, float* pdf, int mf_hemi) {
   switch (b->type) {
     case BSDF_DIFFUSE: /* part1_code.cpp:171-173 */
       *wi = cosine_sample(g, pdf);
@@ -733,6 +738,10 @@ static spec bsdf_sample_f(const bsdf_t* b, rng_t* g, v3 wo, v3* wi, float* pdf) 
       }
     }
     case BSDF_MICROFACET: { /* bsdf.cpp:74-92, MICROFACET_HEMI == 0 */
+      if (mf_hemi) { /* MICROFACET_HEMI == 1 (bsdf.cpp:93-94) */
+        *wi = cosine_sample(g, pdf);
+        return mf_f(b, wo, *wi);
+      }
       double ux, uy;
       grid_sample(g, &ux, &uy);
       float alpha = b->p[6];
@@ -838,10 +847,25 @@ int ro_scene_set_envmap(ro_scene* s, uint32_t w, uint32_t h, const float* texels
 }
 
 /* ------------------------------------------------------------------ lights (light.cpp) */
+static spec light_sample_L_sw(const ro_scene* s, const light_t* l, rng_t* g, v3 p, v3* wi, float* dist, float* pdf,
+                              int env_hemi);
 static spec light_sample_L(const ro_scene* s, const light_t* l, rng_t* g, v3 p, v3* wi, float* dist, float* pdf) {
+  return light_sample_L_sw(s, l, g, p, wi, dist, pdf, 0);
+}
+static spec light_sample_L_sw(const ro_scene* s, const light_t* l, rng_t* g, v3 p, v3* wi, float* dist, float* pdf,
+                              int env_hemi) {
   spec rad = S(l->rad[0], l->rad[1], l->rad[2]);
   switch (l->type) {
     case 5: /* EnvironmentLight */
+      if (env_hemi) { /* ENV_HEMI == 1 (environment_light.cpp:139-142): UniformSphereSampler3D (sampler.cpp:33-40) */
+        *dist = INFINITY;
+        double z = random_uniform(g) * 2 - 1;
+        double q = 1.0f - z * z, sin_t = sqrt(0.0 < q ? q : 0.0);
+        double phi = 2.0f * PI_D * random_uniform(g);
+        *wi = V(cos(phi) * sin_t, sin(phi) * sin_t, z);
+        *pdf = (float)(0.25 / M_PI);
+        return env_dir(s, *wi); /* sample_dir(Ray(p, *wi)) */
+      }
       return env_sample(s, g, wi, dist, pdf);
     case 0: { /* AreaLight::sample_L, light.cpp:80-92 */
       double sx, sy;
@@ -879,6 +903,7 @@ typedef struct {
   const ro_params* p;
   v3 cam_pos, c2w0, c2w1, c2w2;
   double blx, bly;
+  double lens_r, focal;  /* Camera::lensRadius / focalDistance (thin lens) */
 } pctx;
 
 static spec direct_hemisphere(pctx* c, const isect_t* is) { /* :15-31 */
@@ -909,7 +934,7 @@ static spec direct_importance(pctx* c, const isect_t* is) { /* :33-57 */
     total += num;
     for (int i = 0; i < num; ++i) {
       v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L(c->q.s, l, c->q.g, hit_p, &wi_world, &dist, &pdf);
+      spec sample = light_sample_L_sw(c->q.s, l, c->q.g, hit_p, &wi_world, &dist, &pdf, (int)c->p->env_hemi);
       v3 w_in = to_local(X, Y, Z, wi_world);
       if (w_in.z < 0) continue;
       if (!bvh_intersect(&c->q, vadd(hit_p, smul(EPS_D, wi_world)), wi_world, NULL))
@@ -929,10 +954,11 @@ static spec at_least_one_bounce(pctx* c, uint32_t depth, const isect_t* is) { /*
   const bsdf_t* b = &c->q.s->bsdfs[is->bsdf];
   spec L_out = S(0, 0, 0);
   if (!bsdf_is_delta(b)) L_out = sadd(L_out, one_bounce(c, is));
+  if (c->p->illum == 3 && depth == c->p->max_ray_depth) L_out = S(0, 0, 0); /* ILLUM == 3 (:78-81) */
   const double prob = 0.7;
   if (depth == c->p->max_ray_depth || (depth > 1 && coin_flip(c->q.g, prob))) {
     v3 w_in; float pdf;
-    spec sample = bsdf_sample_f(b, c->q.g, w_out, &w_in, &pdf);
+    spec sample = bsdf_sample_f_sw(b, c->q.g, w_out, &w_in, &pdf, (int)c->p->microfacet_hemi);
     if (pdf == 0.0f) return L_out;
     v3 wi_world = to_world(X, Y, Z, w_in);
     isect_t is2;
@@ -949,6 +975,10 @@ static spec est_radiance(pctx* c, v3 o, v3 d) { /* :103-123, ILLUM == 2 */
   isect_t is;
   if (!bvh_intersect(&c->q, o, d, &is)) /* miss: envLight->sample_dir(r), r unbent */
     return c->q.s->env_w ? env_dir(c->q.s, d) : S(0, 0, 0);
+  if (c->p->illum == 0) /* normal_shading (pathtracer.h:199-201) */
+    return sadd(smulf(S((float)is.n.x, (float)is.n.y, (float)is.n.z), (float).5), S(.5f, .5f, .5f));
+  if (c->p->illum == 1) return one_bounce(c, &is);
+  if (c->p->illum == 3) return at_least_one_bounce(c, c->p->max_ray_depth, &is);
   spec e = bsdf_emission(&c->q.s->bsdfs[is.bsdf]);
   if (c->p->max_ray_depth == 0) return e;
   if (c->p->max_ray_depth == 1) return sadd(e, one_bounce(c, &is));
@@ -962,6 +992,16 @@ static void gen_ray(const pctx* c, double x, double y, v3* o, v3* d) { /* Camera
   *d = vunit(w);
 }
 
+static void gen_ray_thin_lens(const pctx* c, double x, double y, double rnd_r, double rnd_theta, v3* o, v3* d) {
+  v3 pin = V((1 - x) * c->blx + x * -c->blx, (1 - y) * c->bly + y * -c->bly, -1);
+  double lr = c->lens_r * sqrt(rnd_r);
+  v3 pl = V(lr * cos(rnd_theta), lr * sin(rnd_theta), 0);
+  /* Matrix3x3 * Vector3D = x[0]*col0 + x[1]*col1 + x[2]*col2 (matrix3x3.cpp:124-128) */
+  *o = vadd(c->cam_pos, vadd(vadd(smul(pl.x, c->c2w0), smul(pl.y, c->c2w1)), smul(pl.z, c->c2w2)));
+  v3 q = vsub(smul(c->focal, pin), pl);
+  *d = vunit(vadd(vadd(smul(q.x, c->c2w0), smul(q.y, c->c2w1)), smul(q.z, c->c2w2)));
+}
+
 static spec raytrace_pixel(pctx* c, uint32_t x, uint32_t y, int32_t* count_out) { /* :125-163 */
   const ro_params* p = c->p;
   spec ret = S(0, 0, 0);
@@ -972,9 +1012,16 @@ static spec raytrace_pixel(pctx* c, uint32_t x, uint32_t y, int32_t* count_out) 
     if (p->ns_aa == 1) { sx += 0.5; sy += 0.5; }
     else { double jx, jy; grid_sample(c->q.g, &jx, &jy); sx += jx; sy += jy; }
     v3 o, d;
-    gen_ray(c, sx / (double)p->frame_w, sy / (double)p->frame_h, &o, &d);
+    if (p->thin_lens) { /* Camera::generate_ray_for_thin_lens (camera.cpp:176-184), part1_code.cpp:137-139 */
+      double lx, ly;
+      grid_sample(c->q.g, &lx, &ly);
+      gen_ray_thin_lens(c, sx / (double)p->frame_w, sy / (double)p->frame_h, lx, ly * 2 * M_PI, &o, &d);
+    } else {
+      gen_ray(c, sx / (double)p->frame_w, sy / (double)p->frame_h, &o, &d);
+    }
     spec s = est_radiance(c, o, d);
     ret = sadd(ret, s);
+    if (!p->adaptive) continue; /* ADAPTIVE == 0 */
     double il = illum(s);
     s1 += il;
     s2 += il * il;
@@ -1000,6 +1047,7 @@ static void pctx_init(pctx* c, const ro_scene* s, const ro_camera* cam, const ro
   /* radians(deg) = deg * (PI / 180) (misc.h:49-52) */
   c->blx = -tan(cam->hFov * (PI_D / 180) / 2);
   c->bly = -tan(cam->vFov * (PI_D / 180) / 2);
+  c->lens_r = cam->lensRadius; c->focal = cam->focalDistance;
 }
 
 /* ------------------------------------------------------------------ tiled thread pool */

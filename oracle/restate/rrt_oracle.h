@@ -53,6 +53,9 @@ typedef struct {
    * build's own; physics pinned by tests/test_kerr_oracle.py): bh_kind 1 = Kerr, spin = a/M */
   uint32_t bh_kind, pad_;
   double bh_spin, bh_axis[3];
+  /* the reference's compile-time switches, defaults as the reference build (pathtracer.h:4-6,
+   * environment_light.h:4, bsdf.h:4) */
+  uint32_t illum, adaptive, thin_lens, env_hemi, microfacet_hemi, pad2_;
 } ro_params;
 void ro_params_default(ro_params* p);
 

@@ -655,8 +655,13 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
 //   direct light;  2 LEAN with point lights too;  V_KERR general with the Kerr march.
 // Each variant is its own kernel build, so no build carries code (and registers) it never runs.
 constexpr int V_KERR = 3;
+// V_SW: the general Schwarzschild build with the reference's compile-time switches as run-time
+// flags (KParams::sw; include/rrt.h RRT_RENDER_THIN_LENS .. RRT_RENDER_ILLUM_MASK)
+constexpr int V_SW = 4;
+enum { SW_THIN_LENS = 1u, SW_NO_ADAPTIVE = 2u, SW_ENV_HEMI = 4u, SW_MF_HEMI = 8u };
+__device__ __forceinline__ uint32_t sw_illum(const KParams& kp) { return ((kp.sw >> 4) & 3u) ^ 2u; }  // ILLUM
 __host__ __device__ constexpr bool is_lean(int v) { return v == 1 || v == 2; }
-__host__ __device__ constexpr int general_of(int v) { return v == V_KERR ? V_KERR : 0; }  // non-LEAN build
+__host__ __device__ constexpr int general_of(int v) { return v == V_KERR || v == V_SW ? v : 0; }  // non-LEAN build
 
 // ------------------------------------------------------------------ Kerr (build-defined)
 // The reference has no Kerr metric; this integrator is this build's design
@@ -1384,7 +1389,7 @@ __device__ __forceinline__ bool refract(v3 wo, v3& wi, float ior) {  // bsdf.cpp
   if (wo.z > 0) wi.z = -wi.z;
   return true;
 }
-__device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf) {
+__device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf, bool mf_hemi = false) {
   switch (b.type) {
     case B_DIFFUSE:
       wi = cosine_sample(g, &pdf);
@@ -1412,6 +1417,10 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf)
       return rf / (float)fabs(wi.z);
     }
     case B_MICROFACET: {
+      if (mf_hemi) {  // MICROFACET_HEMI 1 (bsdf.cpp:93-94): f(wo, *wi = cosine hemisphere sample)
+        wi = cosine_sample(g, &pdf);
+        return mf_f(b, wo, wi);
+      }
       double ux, uy;
       g.grid(ux, uy);
       float alpha = b.p[6];
@@ -1493,7 +1502,8 @@ __device__ __forceinline__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float&
 // ------------------------------------------------------------------ lights (light.cpp)
 // LEAN: every light is an area or a point light
 template <int LEAN = 0>
-__device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf) {
+__device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf,
+                               bool env_hemi = false) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
   switch (LEAN == 1 ? 0u : LEAN == 2 ? (l.type == 1u ? 1u : 0u) : l.type) {
     case 0: {  // AreaLight::sample_L (light.cpp:80-92): float sqDist, sqrtf, float pdf
@@ -1518,6 +1528,16 @@ __device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v
       wi = ld3(l.v[0]); dist = INFINITY; pdf = 1.0f;
       return rad;
     case 5:  // EnvironmentLight (appended by PathTracer::set_scene, pathtracer.cpp:106-108)
+      if (LEAN == V_SW && env_hemi) {  // ENV_HEMI 1 (environment_light.cpp:139-142)
+        dist = INFINITY;
+        // UniformSphereSampler3D::get_sample (sampler.cpp:33-40)
+        const double z = g.uniform() * 2 - 1;
+        const double q = 1.0 - z * z, sin_t = sqrt((0.0 < q) ? q : 0.0);  // std::max(0.0, 1.0f - z * z)
+        const double phi = 2.0 * PI_D * g.uniform();
+        wi = V(rrt_glibm_cos(phi) * sin_t, rrt_glibm_sin(phi) * sin_t, z);
+        pdf = (float)(0.25 / PI_D);
+        return env_dir(env, wi);  // sample_dir(Ray(p, wi))
+      }
       return env_sample(env, g, wi, dist, pdf);
     default: {  // InfiniteHemisphereLight
       v3 dir = hemisphere_sample(g);

@@ -15,6 +15,12 @@
 #include <memory>
 #include <string>
 #include <vector>
+#if RRT_PROFILE
+#include <chrono>
+#include <cstdlib>
+#include <thread>
+#include <unistd.h>
+#endif
 
 #include "../../include/rrt.h"
 #include "../../include/rrt_scene_format.h"
@@ -103,6 +109,10 @@ struct rrt_ctx {
   size_t heavy_list_cap = 0;
   hipStream_t side = nullptr;  // the heavy pixels' kernel runs here, beside the batch kernel
   hipEvent_t ev_go = nullptr, ev_heavy = nullptr;
+#if RRT_PROFILE
+  uint32_t* h_wd = nullptr;  // watchdog progress records (host-coherent, RRT_WATCHDOG_MS)
+  uint32_t* d_wd = nullptr;
+#endif
   bool fenced = false;
   int n_cu = 256;
   // host scene
@@ -128,6 +138,7 @@ struct rrt_ctx {
   double* d_env_marg = nullptr;
   bool has_scene = false, has_camera = false;
   DCamera cam{};
+  double lens_r = 0.0, focal = 0.0;  // Camera::lensRadius / focalDistance (thin lens, RRT_RENDER_THIN_LENS)
   DHole hole{};
   // device scene
   DNode* d_nodes = nullptr;
@@ -993,6 +1004,8 @@ extern "C" int rrt_set_camera(rrt_ctx* c, const rrt_camera_desc* cam) {
   // radians(deg) = deg * (PI / 180) (misc.h:49-52); host libm == the reference's values.
   d.blx = -std::tan(cam->hFov * (kPI / 180) / 2);
   d.bly = -std::tan(cam->vFov * (kPI / 180) / 2);
+  c->lens_r = cam->lensRadius;
+  c->focal = cam->focalDistance;
   c->has_camera = true;
   return RRT_OK;
 }
@@ -1165,6 +1178,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     rrt_ctx* c; hipStream_t s;
     ~FenceGuard() { scratch_release(c, s); }
   } fence_guard{c, stream};
+  // once the heavy pixels' kernel is forked onto the side stream, every path out of here joins it
+  // into `stream` first (so the fence above covers its reads of d_kp / d_counter / the heavy list):
+  // 1 = launched, 2 = its completion event recorded, 3 = joined
+  struct JoinGuard {
+    rrt_ctx* c; hipStream_t s; int state;
+    ~JoinGuard() {
+      if (state == 1) (void)hipStreamSynchronize(c->side);
+      else if (state == 2) (void)hipStreamWaitEvent(s, c->ev_heavy, 0);
+    }
+  } join_guard{c, stream, 0};
   if (c->tiles_cap < n_tiles) {
     // hipFree waits for the device, so no launch still reads the old list
     hipFree(c->d_tiles); c->d_tiles = nullptr;
@@ -1297,15 +1320,26 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // kernel variant (rrt_device.h): the Kerr builds for a Kerr spacetime; else LEAN builds when
   // the scene allows (no environment map, importance-sampled direct light), else general
   const bool kerr = c->hole.kind == RRT_METRIC_KERR;
+  // the reference's compile-time switches (RRT_RENDER_THIN_LENS .. RRT_RENDER_ILLUM_MASK): the
+  // general per-pixel-loop build V_SW (rrt_kernel.hip), every ray marched exactly
+  kp.sw = (p->flags >> 22) & 63u;
+  kp.lens_r = c->lens_r; kp.focal = c->focal;
+  const bool sw = kp.sw != 0;
+  if (sw && kerr) return fail(c, RRT_E_INVALID, "the reference's switches (THIN_LENS, ADAPTIVE, ILLUM, ENV_HEMI, "
+                                                "MICROFACET_HEMI) are built for the Schwarzschild stepper only");
+  if (sw && ((kp.sw >> 4) ^ 2u) == 3u && p->max_ray_depth == 0)
+    return fail(c, RRT_E_INVALID, "ILLUM 3 with max_ray_depth 0 recurses without end in the reference");
+  if (sw) { kp.miss.on = 0u; kp.occ.on = 0u; }
   // bounce paths (depth >= 2): the per-pixel-loop kernel by default; RRT_RENDER_DEEP_SAMPLE selects
   // the per-sample refill kernel (rrt_sample.hip, one lane per pixel, a lane whose pixel is done
   // takes the next at the next sample boundary) -- m3 A/B, profiles/r03_ab_deep.jsonl: 177 ms
   // pixel loop vs 236 ms refill at 3 waves/SIMD, identical outputs
-  const bool deep_sample = deep && !count && !kerr && (p->flags & RRT_RENDER_DEEP_SAMPLE) &&
+  const bool deep_sample = deep && !count && !kerr && !sw && (p->flags & RRT_RENDER_DEEP_SAMPLE) &&
                            !(p->flags & RRT_RENDER_PIXEL_LOOP);
-  const bool pixel_loop = (deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP);
+  const bool pixel_loop = (deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP) || sw;
   const int lean = kerr ? 3 /* V_KERR */
-                        : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
+                 : sw ? 4 /* V_SW */
+                 : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
   const uint32_t wv = p->variant & 0xffu;
   // bounce builds: 3 waves/SIMD (m3 A/B, profiles/r03_ab_deep.jsonl: 363 / 263 / 180 / 180 ms at 1 / 2 / 3 / 4)
   const int waves = (wv >= 1 && wv <= 6) ? (int)wv : deep ? 3 : (pixel_loop ? 2 : 3);
@@ -1459,7 +1493,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
   // centre-first order
   bool deep_list = false;
-  if (deep && !count && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
+  if (deep && !count && !sw && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
       0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
     deep_list = true;
     kp.draws_miss = 2;
@@ -1498,6 +1532,22 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (grid == 0) grid = 1;
   c->last_grid = grid;
+#if RRT_PROFILE
+  // diagnostic build: RRT_WATCHDOG_MS=<ms> gives every batch wave and heavy block a progress record
+  // in host-coherent memory and waits for the launch at most that long; on a stall it prints the
+  // records of the waves that have not exited and ends the process (the hang)
+  const char* wd_env = std::getenv("RRT_WATCHDOG_MS");
+  const long wd_ms = wd_env ? std::atol(wd_env) : 0;
+  if (wd_ms > 0) {
+    if (!c->h_wd) {
+      HIPCHK(c, hipHostMalloc((void**)&c->h_wd, sizeof(uint32_t) * RRT_WD_WORDS, hipHostMallocCoherent | hipHostMallocMapped));
+      HIPCHK(c, hipHostGetDevicePointer((void**)&c->d_wd, c->h_wd, 0));
+    }
+    HIPCHK(c, hipStreamSynchronize(stream));
+    std::memset(c->h_wd, 0, sizeof(uint32_t) * RRT_WD_WORDS);
+    kp.wd = c->d_wd;
+  }
+#endif
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
   HIPCHK(c, hipEventRecord(c->ev0[ring], stream));
@@ -1540,14 +1590,19 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
       HIPCHK(c, hipEventRecord(c->ev_go, stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
+      join_guard.state = 1;
       HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, nw, hgrid, c->side));
       HIPCHK(c, hipEventRecord(c->ev_heavy, c->side));
+      join_guard.state = 2;
     }
     HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, bgrid, stream));
-    if (kp.heavy_list) HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
+    if (kp.heavy_list) {
+      HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
+      join_guard.state = 3;
+    }
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
-                  tf[deep], tf[count], lean == 2 ? 0 : lean);
+                  tf[deep || sw], tf[count], lean == 2 ? 0 : lean);
     if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
@@ -1561,6 +1616,30 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   c->last_kernel = name;
   c->last_heavy = kp.heavy_list ? kp.heavy_cap : 0u;
   HIPCHK(c, hipEventRecord(c->ev1[ring], stream));
+#if RRT_PROFILE
+  if (wd_ms > 0) {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(wd_ms);
+    hipError_t q;
+    while ((q = hipEventQuery(c->ev1[ring])) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (q == hipErrorNotReady) {
+      std::fprintf(stderr, "WATCHDOG: launch '%s' not done after %ld ms (grid %u, heavy list %s); live records:\n",
+                   name, wd_ms, c->last_grid, kp.heavy_list ? "on" : "off");
+      int shown = 0, live_b = 0, live_h = 0;
+      for (uint32_t w = 0; w < RRT_WD_WORDS / 4; ++w) {
+        const volatile uint32_t* r = c->h_wd + 4 * w;
+        if (r[3] == 0 || r[3] == 0xdeadu) continue;
+        if (w < RRT_WD_HEAVY / 4) ++live_b; else ++live_h;
+        if (shown++ < 64)
+          std::fprintf(stderr, "  %s %u: it %u state 0x%x pixel %u marker 0x%x\n", w < RRT_WD_HEAVY / 4 ? "wave" : "heavy",
+                       w < RRT_WD_HEAVY / 4 ? w : w - RRT_WD_HEAVY / 4, r[0], r[1], r[2], r[3]);
+      }
+      std::fprintf(stderr, "WATCHDOG: %d batch waves and %d heavy blocks not exited\n", live_b, live_h);
+      std::fflush(stderr);
+      _exit(3);
+    }
+  }
+#endif
   c->timed = true;
   ++c->n_launch;
   return RRT_OK;
@@ -2054,8 +2133,11 @@ extern "C" int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32
     if (nt == 0) continue;
     int32_t* buf = g->packed[i];
     if (int rc = launch(c, p, tiles[i].data(), nt, ts, x0, y0, x0 + w, y0 + h, (float*)buf, buf + cnt_off, nullptr,
-                        nullptr, c->stream))
+                        nullptr, c->stream)) {
+      // the group reports through member 0's context (rrt_last_error(ctx[0]))
+      if (i > 0) g->ctx[0]->err = "group member " + std::to_string(i) + ": " + c->err;
       return rc;
+    }
     GCHK(g, hipEventRecord(g->ready[i], c->stream));
   }
   // gather to member 0: the frame's only exchange

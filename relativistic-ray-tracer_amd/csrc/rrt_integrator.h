@@ -28,7 +28,8 @@ __device__ spec direct_importance(const KParams& kp, Rng& g, const Isect& is, Co
     total += num;
     for (int i = 0; i < num; ++i) {
       v3 wi_world; float dist, pdf;
-      spec sample = light_sample_L<LEAN>(kp.env, l, g, is.hit_p, wi_world, dist, pdf);
+      spec sample = light_sample_L<LEAN>(kp.env, l, g, is.hit_p, wi_world, dist, pdf,
+                                         LEAN == V_SW && (kp.sw & SW_ENV_HEMI));
       const Frame f = coord_space(is.n);
       v3 w_in = to_local(f, wi_world);
       if (w_in.z < 0) continue;
@@ -78,12 +79,13 @@ __device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, I
     const DBsdf b = kp.bsdfs[cur.bsdf];
     spec L_out = S(0, 0, 0);
     if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, general_of(LEAN), true>(kp, g, cur, cn);
+    if (LEAN == V_SW && sw_illum(kp) == 3u && depth == kp.max_ray_depth) L_out = S(0, 0, 0);  // ILLUM 3 (:78-81)
     Ld[k] = L_out;
     child[k] = false;
     dl[k] = is_delta(b);
     if (depth == kp.max_ray_depth || (depth > 1 && g.coin(0.7))) {
       v3 w_in; float pdf;
-      spec sample = bsdf_sample_f(b, g, w_out, w_in, pdf);
+      spec sample = bsdf_sample_f(b, g, w_out, w_in, pdf, LEAN == V_SW && (kp.sw & SW_MF_HEMI));
       if (pdf == 0.0f) break;
       v3 wi_world = to_world(f, w_in);
       Isect is2;

@@ -205,4 +205,17 @@ struct KParams {
   double heavy_r2;        // (RRT_HEAVY_NEAR x r_s)^2: rays passing this close make a pixel heavy
   uint64_t free_big_mask; // oversized leaves traverse_free tests from its list (the others are in
                           // the search tree); ~0 for the clean-tree and reference-tree walks
+  // the reference's compile-time switches as run-time flags (include/rrt.h RRT_RENDER_THIN_LENS ..
+  // RRT_RENDER_ILLUM_MASK; kernel variant V_SW only): flag bits 22..27 >> 22, the camera's lens
+  double lens_r, focal;   // Camera::lensRadius / focalDistance (camera.cpp:176-184)
+  uint32_t sw;            // bit 0 thin lens, 1 no adaptive, 2 env hemi, 3 microfacet hemi, 4..5 ILLUM ^ 2
+  uint32_t sw_pad;
+#if RRT_PROFILE
+  // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
+  // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves
+  // first, the heavy kernel's blocks from RRT_WD_HEAVY on
+  uint32_t* wd;
+#endif
 };
+#define RRT_WD_WORDS (1u << 18)
+#define RRT_WD_HEAVY (1u << 17)

@@ -17,13 +17,20 @@ __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3
   if (camera_proven_miss<COUNT, LEAN == V_KERR, LEAN == 0, W>(kp, o, d, cn) ||
       !trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
     return (!is_lean(LEAN) && kp.env.w) ? env_dir(kp.env, d) : S(0, 0, 0);
+  if (LEAN == V_SW && sw_illum(kp) != 2u) {  // ILLUM 0 / 1 / 3 (:108-122)
+    const uint32_t il = sw_illum(kp);
+    if (il == 0u)  // normal_shading (pathtracer.h:199-201): Spectrum(n) * .5 + Spectrum(.5, .5, .5)
+      return S((float)is.n.x, (float)is.n.y, (float)is.n.z) * (float).5 + S(.5f, .5f, .5f);
+    if (il == 1u) return one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
+    return at_least_one_bounce<COUNT, LEAN>(kp, g, is, cn);
+  }
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
   if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
   return e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
 }
 
-// PathTracer::raytrace_pixel (:125-163) with ADAPTIVE == 1, THIN_LENS == 0
+// PathTracer::raytrace_pixel (:125-163): ADAPTIVE 1, THIN_LENS 0 -- or, in the V_SW build, as kp.sw says
 template <bool DEEP, bool COUNT, int LEAN, int W = 0>
 __device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
   spec ret = S(0, 0, 0);
@@ -35,12 +42,27 @@ __device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, ui
     double sx = (double)x, sy = (double)y;
     if (kp.ns_aa == 1) { sx += 0.5; sy += 0.5; }
     else { double jx, jy; g.grid(jx, jy); sx += jx; sy += jy; }
-    // Camera::generate_ray (part1_code.cpp:182-187)
     double cx = sx / kp.frame_w, cy = sy / kp.frame_h;
     double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
-    v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
-    spec s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, ld3(cam.pos), unit(w), cn);
+    spec s;
+    if (LEAN == V_SW && (kp.sw & SW_THIN_LENS)) {
+      // Camera::generate_ray_for_thin_lens (camera.cpp:176-184) at the lens sample the grid sampler
+      // draws after the jitter (part1_code.cpp:137-139): rndR = its x, rndTheta = its y * 2 * M_PI
+      double lx, ly; g.grid(lx, ly);
+      const double rnd_theta = ly * 2 * PI_D;
+      const double lr = kp.lens_r * sqrt(lx);
+      const v3 pl = V(lr * rrt_glibm_cos(rnd_theta), lr * rrt_glibm_sin(rnd_theta), 0);
+      const v3 c0 = ld3(cam.c2w0), c1 = ld3(cam.c2w1), c2 = ld3(cam.c2w2);
+      const v3 o = ld3(cam.pos) + ((smul(pl.x, c0) + smul(pl.y, c1)) + smul(pl.z, c2));  // pos + c2w * pLens
+      const v3 q = V(vx * kp.focal, vy * kp.focal, -1.0 * kp.focal) - pl;                // pinHole * f - pLens
+      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, o, unit((smul(q.x, c0) + smul(q.y, c1)) + smul(q.z, c2)), cn);
+    } else {
+      // Camera::generate_ray (part1_code.cpp:182-187)
+      v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
+      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, ld3(cam.pos), unit(w), cn);
+    }
     ret = ret + s;
+    if (LEAN == V_SW && (kp.sw & SW_NO_ADAPTIVE)) { n = i + 1; continue; }  // ADAPTIVE 0
     double il = illum(s);
     s1 += il;
     s2 += il * il;
@@ -165,7 +187,9 @@ __global__ void rrt_libm_kernel(int fn, uint64_t n, const double* a, const doubl
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream) {
 #define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
-  if (lean == rrt::V_KERR) {  // the Kerr builds (general integrator)
+  if (lean == rrt::V_SW) {  // the reference's switches as run-time flags: one bounce-capable build
+    if (count) RRT_LAUNCH(true, true, rrt::V_SW, 1); else RRT_LAUNCH(true, false, rrt::V_SW, 1);
+  } else if (lean == rrt::V_KERR) {  // the Kerr builds (general integrator)
     if (deep) {
       if (count) RRT_LAUNCH(true, true, rrt::V_KERR, 1); else RRT_LAUNCH(true, false, rrt::V_KERR, 1);
     } else if (count) {

@@ -489,16 +489,26 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
   Counters cn = {};
   const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
   __builtin_amdgcn_s_setprio(3);
+#if RRT_PROFILE
+  volatile uint32_t* wd = kp.wd ? kp.wd + RRT_WD_HEAVY + 4u * (blockIdx.x & 0x7fffu) : nullptr;
+  uint32_t wd_it = 0;
+#endif
   for (;;) {
     if (t == 0) hl.hx = atomicAdd(kp.heavy_count + 1, 1u);
     __syncthreads();
     const uint32_t k = hl.hx;
     __syncthreads();  // every thread has read it before thread 0 claims again
+#if RRT_PROFILE
+    if (wd && t == 0) { wd[0] = ++wd_it; wd[1] = nh; wd[2] = k; wd[3] = 0x11u; }
+#endif
     if (k >= nh) break;
 #if RRT_PROFILE
     const uint64_t w_h = wall_clock64();
 #endif
     heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl, t, k, cn);
+#if RRT_PROFILE
+    if (wd && t == 0) wd[3] = 0x12u;  // pixel done
+#endif
 #if RRT_PROFILE  // elapsed ticks; "rounds" 1
     if (t == 0) {
       const uint32_t ts = kp.tile_size, tpix = ts * ts;
@@ -507,6 +517,9 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
     }
 #endif
   }
+#if RRT_PROFILE
+  if (wd && t == 0) wd[3] = 0xdeadu;  // exited
+#endif
 }
 
 // waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks
@@ -560,8 +573,15 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
 
   uint64_t t_claim = 0;  // when the group claimed its pixel (wall clock)
+#if RRT_PROFILE
+  volatile uint32_t* wd = kp.wd ? kp.wd + 4u * ((blockIdx.x * (blockDim.x >> 6) + (t >> 6)) & 0x7fffu) : nullptr;
+  uint32_t wd_it = 0;
+#endif
 
   for (;;) {
+#if RRT_PROFILE
+    if (wd && lane == 0) { wd[0] = ++wd_it; wd[1] = (have ? 1u : 0u) | (done ? 2u : 0u); wd[3] = 0x21u; }
+#endif
     // ---- claim a pixel (one atomic per group)
     RRT_T0(tc0);
     // The wave's group leaders that need a pixel claim together: one atomic takes as many
@@ -726,6 +746,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     bool resolved = !have;      // (group-uniform)
     for (int round = 0;; ++round) {
       const bool need = my < RRT_SLOTS;
+#if RRT_PROFILE
+      if (wd && lane == 0) { wd[1] = (have ? 1u : 0u) | (done ? 2u : 0u) | ((uint32_t)round << 8); wd[2] = lget(gs.slot, gid); wd[3] = 0x22u; }
+#endif
       if (__ballot(need) == 0) break;
       if (round > 0) tail_prio();
 #if RRT_PROFILE
@@ -911,6 +934,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     if (stop) have = false;
     RRT_ACC(t_fold, tf0);
   }
+#if RRT_PROFILE
+  if (wd && lane == 0) wd[3] = 0xdeadu;  // exited
+#endif
 #if RRT_PROFILE
   const uint64_t t_end = clock64(), w_end = wall_clock64();
   uint64_t v[12] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0,

@@ -28,6 +28,13 @@ RRT_RENDER_ONE_QUEUE, RRT_RENDER_XCD_QUEUES, RRT_RENDER_NO_MISS_PROOF, RRT_RENDE
 RRT_RENDER_STRIPED_QUEUES, RRT_RENDER_NO_SHADOW_PROOF, RRT_RENDER_NO_PIXEL_PROOF = 1 << 15, 1 << 16, 1 << 17
 RRT_RENDER_NO_SEARCH_TREE, RRT_RENDER_DEEP_SAMPLE, RRT_RENDER_NO_HEAVY, RRT_RENDER_HEAVY = 1 << 18, 1 << 19, 1 << 20, 1 << 21
 RRT_RENDER_DIAG_NO_TRAVERSE, RRT_RENDER_DIAG_CLEAR_STATS = 1 << 30, 1 << 31
+# the reference's compile-time switches (pathtracer.h:4-6, environment_light.h:4, bsdf.h:4) as flags
+RRT_RENDER_THIN_LENS, RRT_RENDER_NO_ADAPTIVE, RRT_RENDER_ENV_HEMI, RRT_RENDER_MICROFACET_HEMI = 1 << 22, 1 << 23, 1 << 24, 1 << 25
+
+
+def RRT_RENDER_ILLUM(n):
+    """ILLUM n (pathtracer.h:4) as flag bits 26..27 (ILLUM 2, the default: 0)."""
+    return ((n ^ 2) & 3) << 26
 
 
 class RRTError(RuntimeError):

@@ -31,7 +31,9 @@ class Params(C.Structure):
                 ("direct_hemisphere", C.c_uint32), ("seed", C.c_uint64), ("frame_w", C.c_uint32),
                 ("frame_h", C.c_uint32), ("bh_center", C.c_double * 3), ("bh_radius", C.c_double),
                 ("bh_dtheta", C.c_double), ("bh_kind", C.c_uint32), ("pad_", C.c_uint32), ("bh_spin", C.c_double),
-                ("bh_axis", C.c_double * 3)]
+                ("bh_axis", C.c_double * 3), ("illum", C.c_uint32), ("adaptive", C.c_uint32),
+                ("thin_lens", C.c_uint32), ("env_hemi", C.c_uint32), ("microfacet_hemi", C.c_uint32),
+                ("pad2_", C.c_uint32)]
 
 
 _lib = None
@@ -118,8 +120,12 @@ def load_camera(path):
 
 
 def make_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, samples_per_batch=32,
-                max_tolerance=0.05, direct_hemisphere=False, seed=0, bh=(0.0, 1.0, 0.0, 0.1, 0.1), kerr=None):
-    """kerr: None (Schwarzschild) or (spin a/M, (ax, ay, az)) for the build-defined Kerr integrator."""
+                max_tolerance=0.05, direct_hemisphere=False, seed=0, bh=(0.0, 1.0, 0.0, 0.1, 0.1), kerr=None,
+                illum=2, adaptive=True, thin_lens=False, env_hemi=False, microfacet_hemi=False):
+    """kerr: None (Schwarzschild) or (spin a/M, (ax, ay, az)) for the build-defined Kerr integrator.
+    illum / adaptive / thin_lens / env_hemi / microfacet_hemi: the reference's compile-time switches
+    (ILLUM, ADAPTIVE, THIN_LENS pathtracer.h:4-6, ENV_HEMI environment_light.h:4, MICROFACET_HEMI
+    bsdf.h:4), defaults as the reference build."""
     p = Params()
     lib().ro_params_default(C.byref(p))
     p.ns_aa, p.max_ray_depth, p.ns_area_light = ns_aa, max_ray_depth, ns_area_light
@@ -130,6 +136,8 @@ def make_params(frame_w, frame_h, ns_aa=1, max_ray_depth=1, ns_area_light=1, sam
     if kerr is not None:
         p.bh_kind, p.bh_spin = 1, kerr[0]
         p.bh_axis[0], p.bh_axis[1], p.bh_axis[2] = kerr[1]
+    p.illum, p.adaptive, p.thin_lens = illum, int(adaptive), int(thin_lens)
+    p.env_hemi, p.microfacet_hemi = int(env_hemi), int(microfacet_hemi)
     return p
 
 

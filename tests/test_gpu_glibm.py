@@ -71,9 +71,9 @@ def test_random_arguments(gpu):
     g = np.random.default_rng(20261017)
     n = 1 << 22
 
-    def mixed(lim):  # half value-uniform, half log-uniform magnitude, either sign
+    def mixed(lim):  # half value-uniform, half log-uniform magnitude (60 octaves below lim), either sign
         v = g.uniform(-lim, lim, n)
-        e = g.uniform(-60, np.log2(lim), n)
+        e = g.uniform(min(-60.0, np.log2(lim) - 60.0), np.log2(lim), n)
         v[: n // 2] = np.sign(g.uniform(-1, 1, n // 2)) * 2.0 ** e[: n // 2]
         return v
 

@@ -51,6 +51,15 @@ for step in "$@"; do
     cache) run pmc_lat 600 rocprofv3 --pmc TCP_TCP_LATENCY_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --kernel-trace -d gpurun_out/pmc_lat -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0} ;;
+    hang)  # diagnostic build with the watchdog (RRT_WATCHDOG_MS): the round-3 profile-build hang case
+           run hang_b1 180 env RRT_LIB=tools/librrt_prof_wd.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
+           run hang_cfg3 180 env RRT_LIB=tools/librrt_prof_wd.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540 ;;
+    hang_nowd)  # the same diagnostic build without the watchdog (round 3's exact command shape)
+           run hang_b1_nowd 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
+           run hang_cfg3_nowd 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540
+           run hang_cfg3_full 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 2097152 ;;
+    prof8) # kernel trace of every rank's tile set of the 8-way cfg3 split (batch vs heavy kernel per launch)
+           run prof8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 ;;
     kerr)  run pytest_kerr 600 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 300 --timeout-method thread ;;
     cli)   run pytest_cli 600 python3 -u -m pytest tests/test_gpu_cli.py -x -q -s --timeout 300 --timeout-method thread ;;
     abw)   run abw 900 python3 tools/ab_workload.py --workload ${AB_WORKLOAD:-cfg5} --rounds ${AB_ROUNDS:-2} ${AB_WVARIANTS:-0 0:2048} ;;
