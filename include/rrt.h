@@ -29,7 +29,8 @@ extern "C" {
 #define RRT_ABI_VERSION 3  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
                               3: rrt_stats gained last_main_kernel_ms / last_heavy_pixels (callers
                                  built against 2 pass a smaller struct: rebuild), the
-                                 RRT_RENDER_WAVEFRONT flag is rejected (RRT_E_INVALID),
+                                 RRT_RENDER_WAVEFRONT selects the path pool kernel (depth >= 2;
+                                 RRT_E_INVALID elsewhere),
                                  rrt_libm_eval added */
 
 enum {
@@ -174,7 +175,10 @@ typedef struct {
 enum {
   RRT_RENDER_COUNTERS = 1u << 0, /* also produce per-pixel work counters (slower variant) */
   RRT_RENDER_DRAWS = 1u << 1,    /* also produce per-pixel RNG draw counts */
-  RRT_RENDER_WAVEFRONT = 1u << 2, /* removed (round 3; it lost every A/B): rejected with RRT_E_INVALID */
+  RRT_RENDER_WAVEFRONT = 1u << 2, /* depth >= 2 (Schwarzschild): the path pool kernel -- one ray per
+                                     lane per round, the paths' state between rays in LDS -- instead
+                                     of the per-pixel loop (A/B, slower on m3); RRT_E_INVALID with
+                                     Kerr, counters, switches or depth <= 1 */
   RRT_RENDER_EXACT_DIV = 1u << 3, /* slab tests by true division instead of the
                                      Markstein-corrected reciprocal (A/B testing) */
   RRT_RENDER_PIXEL_LOOP = 1u << 4, /* depth <= 1: per-pixel-loop kernel instead of the default

@@ -403,7 +403,7 @@ __device__ __forceinline__ int next_big_in(uint64_t m, int from, int nb) {
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool traverse_free(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
                                               double& hb1, double& hb2, Counters& cn, bool exact,
-                                              uint64_t bmask = ~0ull) {
+                                              uint64_t bmask = ~0ull, bool any_rt = false) {
   if (COUNT) cn.bbox++;
   if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return false;
   bmask &= kp.free_big_mask;  // the local oversized leaves sit in the search tree
@@ -455,7 +455,7 @@ __device__ __forceinline__ bool traverse_free(const KParams& kp, v3 o, v3 d, v3 
           const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, L, t)
                                       : tri_t(gp, o, d, L, t, b1, b2);
           if (!ok) continue;
-          if (ANY) return true;
+          if (ANY || any_rt) return true;
           if (na == 4) {  // keep the 4 smallest
             more = true;
             if (slot > s3) continue;
@@ -591,9 +591,10 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
 // One micro segment (o, d, max_t) against the scene -- BVHAccel::intersect_micro (bvh.cpp:115-138)
 // behind the result-identical skips -- filling *is on a hit.  Shared by the
 // Schwarzschild march below and the Kerr march (query_kerr).
+// any_rt: a shadow query chosen at run time (the path pool kernel's rays share one query call)
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, v3 e, Isect* is,
-                                              Counters& cn) {
+                                              Counters& cn, bool any_rt = false) {
   // e = o + d * max_t.  COUNT && kp.count_exec: count the work this path executes (grid / root
   // skips, clean walk, plane tests in the query slot) instead of the reference's
   const bool opt = !COUNT || kp.count_exec;
@@ -620,7 +621,7 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   RRT_T0(tt0);
   bool hit;
   if (!COUNT)  // the search tree (or, for A/B, the clean tree or the reference tree itself)
-    hit = traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
+    hit = traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt);
   else if (kp.count_exec)
     hit = traverse_free<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
   else
@@ -631,7 +632,7 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
 #endif
   if (COUNT && (kp.diag & 2)) cn.prim = prim_before + (clear_diag ? 0u : cn.bbox - bbox_before);
   if (!hit) return false;
-  if (!ANY) {
+  if (!ANY && !any_rt) {
     const DPrimMeta meta = kp.meta[slot];
     is->bsdf = (int)((meta >> 8) & 0xffu);
     is->hit_p = o + vmul(d, seg_t);
@@ -970,8 +971,11 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
 #else
 #define RRT_QACC(v)
 #endif
+#ifndef RRT_QUERY_ATTR  // a translation unit may force the query inline (rrt_path.hip)
+#define RRT_QUERY_ATTR __device__
+#endif
 template <bool ANY, bool COUNT, bool KERR = false>
-__device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn, bool any_rt = false) {
   if (KERR) return query_kerr<ANY, COUNT>(kp, o, d, is, cn);
   if (COUNT && !kp.count_exec && !(kp.diag & 2)) cn.query++;
   RRT_T0(tq0);
@@ -989,7 +993,7 @@ __device__ bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
       return false;
     }
     e = o + vmul(d, max_t);
-    if (segment_query<ANY, COUNT>(kp, o, d, max_t, e, is, cn)) {
+    if (segment_query<ANY, COUNT>(kp, o, d, max_t, e, is, cn, any_rt)) {
       RRT_QACC(tq0);
       return true;
     }

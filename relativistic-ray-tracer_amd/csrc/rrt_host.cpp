@@ -34,6 +34,7 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream);
 hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_path(const KParams* d_kp, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
 hipError_t rrt_launch_libm(int fn, uint64_t n, const double* a, const double* b, double* out, hipStream_t stream);
@@ -107,6 +108,8 @@ struct rrt_ctx {
   // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
   uint32_t* d_heavy_list = nullptr;
   size_t heavy_list_cap = 0;
+  float* d_path_stack = nullptr;  // the path pool kernel's per-level terms (rrt_path.hip)
+  size_t path_stack_cap = 0;      // bytes
   hipStream_t side = nullptr;  // the heavy pixels' kernel runs here, beside the batch kernel
   hipEvent_t ev_go = nullptr, ev_heavy = nullptr;
 #if RRT_PROFILE
@@ -276,6 +279,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_list); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     hipFree(c->d_heavy_list);
+    hipFree(c->d_path_stack);
     for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
       if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
       if (c->ev_main[i]) hipEventDestroy(c->ev_main[i]);
@@ -1314,9 +1318,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // builds when the scene allows them; variant = register budget in waves per SIMD.
   const int deep = p->max_ray_depth >= 2 ? 1 : 0;
   const int count = (p->flags & RRT_RENDER_COUNTERS) && d_ctr ? 1 : 0;
-  // the wavefront state-machine kernel (rrt_mega.hip, an A/B variant that lost every measurement,
-  // DESIGN.md §5) was removed in round 3: its flag is rejected
-  if (p->flags & RRT_RENDER_WAVEFRONT) return fail(c, RRT_E_INVALID, "the wavefront A/B kernel was removed");
   // kernel variant (rrt_device.h): the Kerr builds for a Kerr spacetime; else LEAN builds when
   // the scene allows (no environment map, importance-sampled direct light), else general
   const bool kerr = c->hole.kind == RRT_METRIC_KERR;
@@ -1336,13 +1337,22 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // pixel loop vs 236 ms refill at 3 waves/SIMD, identical outputs
   const bool deep_sample = deep && !count && !kerr && !sw && (p->flags & RRT_RENDER_DEEP_SAMPLE) &&
                            !(p->flags & RRT_RENDER_PIXEL_LOOP);
-  const bool pixel_loop = (deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP) || sw;
+  // RRT_RENDER_WAVEFRONT: the bounce paths (depth >= 2, Schwarzschild) in the path pool kernel
+  // (rrt_path.hip: one ray per lane per round, the paths' integrator state between rays in LDS),
+  // an A/B variant: m3 269 ms at 3 waves/SIMD vs 172 ms for the per-pixel loop.
+  // Its light-sample cursor holds 11 bits: n_lights x ns_area_light < 2048.
+  const bool path_pool = (p->flags & RRT_RENDER_WAVEFRONT) != 0;
+  if (path_pool && !(deep && !count && !kerr && !sw && p->ns_aa >= 1 &&
+                     (uint64_t)all_lights(c).size() * std::max<uint32_t>(1u, p->ns_area_light) < 2048u))
+    return fail(c, RRT_E_INVALID, "RRT_RENDER_WAVEFRONT (the path pool kernel) renders max_ray_depth >= 2 "
+                                  "Schwarzschild frames without counters or switches, n_lights x ns_area_light < 2048");
+  const bool pixel_loop = !path_pool && ((deep && !deep_sample) || (p->flags & RRT_RENDER_PIXEL_LOOP) || sw);
   const int lean = kerr ? 3 /* V_KERR */
                  : sw ? 4 /* V_SW */
                  : (!deep && !count && !c->env_w && !p->direct_hemisphere) ? c->lean : 0;
   const uint32_t wv = p->variant & 0xffu;
   // bounce builds: 3 waves/SIMD (m3 A/B, profiles/r03_ab_deep.jsonl: 363 / 263 / 180 / 180 ms at 1 / 2 / 3 / 4)
-  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : deep ? 3 : (pixel_loop ? 2 : 3);
+  const int waves = (wv >= 1 && wv <= 6) ? (int)wv : path_pool ? RRT_PATH_WAVES : deep ? 3 : (pixel_loop ? 2 : 3);
   // persistent grid, 4 waves per block, up to 8 blocks per CU (the 32-wave limit): as many
   // blocks as the kernel's registers allow become resident; any others start when a resident
   // block exits and find the atomic work counter exhausted
@@ -1481,9 +1491,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         kp.heavy_list = c->d_heavy_list;
         kp.heavy_count = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);
         kp.heavy_cap = cap;
-        // A/B (variant bits 16..19): 1: capture-boundary pixels only, 2 / 3 / 4: near 1.1 / 1.5 / 2.0
+        // A/B (variant bits 16..19): 1: capture-boundary pixels only, 2 .. 6: near 1.1 / 1.5 / 2.0 / 3.0 / 5.0
         const uint32_t nv = (p->variant >> 16) & 0xfu;
-        const double near = nv == 1 ? 0.0 : nv == 2 ? 1.1 : nv == 3 ? 1.5 : nv == 4 ? 2.0 : RRT_HEAVY_NEAR;
+        const double near = nv == 1 ? 0.0 : nv == 2 ? 1.1 : nv == 3 ? 1.5 : nv == 4 ? 2.0 : nv == 5 ? 3.0 : nv == 6 ? 5.0 : RRT_HEAVY_NEAR;
         kp.heavy_r2 = (near * c->hole.r) * (near * c->hole.r);
       }
     }
@@ -1492,10 +1502,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // pixel's samples all miss at any depth (est_radiance returns the black miss, 2 draws each), so
   // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
   // centre-first order
-  bool deep_list = false;
-  if (deep && !count && !sw && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
-      0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 && !(p->flags & RRT_RENDER_NO_PIXEL_PROOF)) {
-    deep_list = true;
+  // The path pool kernel claims from the same centre-first order, listed or not.
+  const bool deep_list = deep && !count && !sw && proofs_valid && !c->env_w && !kerr && kp.miss.on &&
+                         0.0 <= (double)p->max_tolerance * 0.0 && p->samples_per_batch >= 2 &&
+                         !(p->flags & RRT_RENDER_NO_PIXEL_PROOF);
+  if (deep_list || path_pool) {
     kp.draws_miss = 2;
     kp.n_pixels = n_tiles * ts * ts;
     std::vector<uint32_t> order(n_tiles);
@@ -1520,16 +1531,31 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       HIPCHK(c, hipMemcpyAsync(c->d_order, c->h_order.data(), sizeof(uint32_t) * n_tiles, hipMemcpyHostToDevice, stream));
     }
     kp.tile_order = c->d_order;
-    if (c->list_cap < kp.n_pixels) {
-      hipFree(c->d_list); c->d_list = nullptr;
-      HIPCHK(c, hipMalloc(&c->d_list, sizeof(uint32_t) * kp.n_pixels));
-      c->list_cap = kp.n_pixels;
+    if (deep_list) {
+      if (c->list_cap < kp.n_pixels) {
+        hipFree(c->d_list); c->d_list = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_list, sizeof(uint32_t) * kp.n_pixels));
+        c->list_cap = kp.n_pixels;
+      }
+      kp.claim_list = c->d_list;
+      kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
     }
-    kp.claim_list = c->d_list;
-    kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
   }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
+  if (path_pool) {  // 256 paths a block, the resident blocks only (each path holds a stack slot)
+    const uint32_t pw = (waves >= 2 && waves <= 4) ? (uint32_t)waves : (uint32_t)RRT_PATH_WAVES;
+    grid = std::min<uint32_t>((kp.n_pixels + 255u) / 256u, (uint32_t)c->n_cu * pw);
+    if (grid == 0) grid = 1;
+    // levels 0 .. max_ray_depth - 1 of the recursion, then each path's pixel record
+    const size_t bytes = sizeof(float) * RRT_PATH_FIELDS * ((size_t)p->max_ray_depth + 1u) * grid * 256u;
+    if (c->path_stack_cap < bytes) {
+      hipFree(c->d_path_stack); c->d_path_stack = nullptr; c->path_stack_cap = 0;
+      HIPCHK(c, hipMalloc(&c->d_path_stack, bytes));
+      c->path_stack_cap = bytes;
+    }
+    kp.path_stack = c->d_path_stack;
+  }
   if (grid == 0) grid = 1;
   c->last_grid = grid;
 #if RRT_PROFILE
@@ -1548,6 +1574,20 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     kp.wd = c->d_wd;
   }
 #endif
+  // the heavy pixels' kernel (batch launches with a heavy list): its waves per pixel and grid, and
+  // whether the batch kernel sizes its room for it on the device (variant bits 22 / 23: A/B)
+  const uint32_t hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
+  const int heavy_nw = nwv == 0 ? 2 : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;  // waves per heavy pixel
+  // heavy waves: hgv x the CU count (default 2), in blocks of heavy_nw waves
+  const uint32_t heavy_waves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
+  const uint32_t heavy_grid = std::max<uint32_t>(1u, heavy_waves / (uint32_t)heavy_nw);
+  const bool no_room = (p->variant >> 23) & 1u;      // A/B: leave the batch grid as it is
+  // A/B: round 3's fixed room, of (variant bits 12..15) - 1 blocks per CU beyond the heavy waves
+  const bool static_room = ((p->variant >> 12) & 0xfu) != 0u;
+  if (batch && kp.heavy_list && !no_room && !static_room) {
+    kp.heavy_grid = heavy_grid;
+    kp.heavy_nw = (uint32_t)heavy_nw;
+  }
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
   HIPCHK(c, hipEventRecord(c->ev0[ring], stream));
@@ -1578,16 +1618,21 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       // hardware queue), after the pass, beside the batch kernel; the batch grid leaves room for
       // its blocks (one per CU at most, <= 128 VGPRs and 23 KB of LDS next to four batch blocks),
       // whichever kernel the hardware dispatches first
-      const uint32_t hwv = (p->variant >> 24) & 0xfu, hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
+      const uint32_t hwv = (p->variant >> 24) & 0xfu;
       const int hw = hwv == 5 ? 5 : 4;
-      const int nw = nwv == 0 ? 2 : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;  // waves per heavy pixel
-      // heavy waves: hgv x the CU count (default 2), in blocks of nw waves
-      const uint32_t hwaves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
-      const uint32_t hgrid = std::max<uint32_t>(1u, hwaves / (uint32_t)nw);
+      const int nw = heavy_nw;
+      const uint32_t hgrid = heavy_grid;
       const uint32_t resident = (uint32_t)c->n_cu * (uint32_t)(lean == 1 || lean == 2 ? w : gw);  // blocks of 4 waves
-      const uint32_t spare = ((p->variant >> 12) & 0xfu) * (uint32_t)c->n_cu + (hwaves + 3u) / 4u;  // room, in batch blocks
-      const bool no_room = (p->variant >> 23) & 1u;  // A/B: leave the batch grid as it is
-      if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
+      const uint32_t spare = (static_room ? ((p->variant >> 12) & 0xfu) - 1u : 0u) * (uint32_t)c->n_cu +
+                             (heavy_waves + 3u) / 4u;  // room, in batch blocks
+      if (static_room) {
+        if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
+      } else if (!no_room) {
+        // room sized on the device to the heavy pixels the pass found (rrt_batch_kernel prologue,
+        // kp.heavy_grid / heavy_nw): the grid is exactly the resident blocks, so a block that
+        // leaves frees a slot no pending batch block can take
+        bgrid = std::min(bgrid, resident);
+      }
       HIPCHK(c, hipEventRecord(c->ev_go, stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
       join_guard.state = 1;
@@ -1600,6 +1645,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
       join_guard.state = 3;
     }
+  } else if (path_pool) {
+    std::snprintf(name, sizeof(name), "%srrt_path_kernel<%d>", deep_list ? "rrt_pixel_proof_kernel + " : "",
+                  (waves >= 2 && waves <= 4) ? waves : RRT_PATH_WAVES);
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
+    HIPCHK(c, rrt_launch_path(c->d_kp, waves, grid, stream));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   tf[deep || sw], tf[count], lean == 2 ? 0 : lean);

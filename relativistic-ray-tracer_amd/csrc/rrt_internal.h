@@ -6,6 +6,8 @@
 #define RRT_MAX_LIGHTS 16
 #define RRT_MAX_BSDFS 64
 #define RRT_MAX_DEPTH 16
+#define RRT_PATH_FIELDS 13  // the path pool kernel's stack: words per recursion level (rrt_path.hip)
+#define RRT_PATH_WAVES 4    // ... and its default register budget (waves per SIMD)
 #define RRT_BIG_REACH 10   // oversized-leaf cell masks: dilation radius in grid cells (rrt_host.cpp)
 
 // BVH node, 64 B, left-first pre-order (the reference's recursion order, bvh.cpp:115-138).
@@ -209,7 +211,13 @@ struct KParams {
   // RRT_RENDER_ILLUM_MASK; kernel variant V_SW only): flag bits 22..27 >> 22, the camera's lens
   double lens_r, focal;   // Camera::lensRadius / focalDistance (camera.cpp:176-184)
   uint32_t sw;            // bit 0 thin lens, 1 no adaptive, 2 env hemi, 3 microfacet hemi, 4..5 ILLUM ^ 2
+  // the heavy pixels' kernel beside the batch kernel: its grid (blocks of heavy_nw waves); the
+  // batch kernel's top blocks make room for as many of them as there are heavy pixels (0: none)
+  uint32_t heavy_grid, heavy_nw;
   uint32_t sw_pad;
+  // the path pool kernel (rrt_path.hip, depth >= 2): each path's per-level terms of
+  // at_least_one_bounce_radiance, [level][field][path] (RRT_PATH_FIELDS floats a level)
+  float* path_stack;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

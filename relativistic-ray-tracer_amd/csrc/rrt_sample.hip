@@ -569,6 +569,16 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   uint32_t px_rounds = 0, px_steps = 0;           // of the group's current pixel
 #endif
 
+  // Room for the heavy pixels' kernel (launched beside this one on the side stream): the grid is
+  // the resident block count, and its top blocks -- as many as the heavy pixels the pass listed
+  // need, in batch blocks of 4 waves -- leave at once, so the heavy kernel's blocks take their
+  // slots whichever kernel the hardware dispatched first.  A launch with no heavy pixels keeps
+  // every block (the heavy kernel's blocks then start at its end and find the list empty).
+  if (kp.heavy_grid) {
+    const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
+    const uint32_t need = (min(nh, kp.heavy_grid) * kp.heavy_nw + 3u) / 4u;
+    if (blockIdx.x + min(need, gridDim.x - 1u) >= gridDim.x) return;
+  }
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
 

@@ -100,9 +100,9 @@ def test_kerr_differs_from_schwarzschild(gpu):
     assert np.array_equal(s_rgb.view(np.uint32), c.px["rgb"].view(np.uint32))
 
 
-def test_removed_wavefront_flag_is_rejected(gpu):
-    """The wavefront A/B kernel (round 1-2, slower in every measurement) is gone from the library;
-    its flag fails loudly instead of silently running another kernel."""
+def test_wavefront_flag_is_rejected_for_kerr(gpu):
+    """RRT_RENDER_WAVEFRONT selects the path pool kernel (depth >= 2, Schwarzschild only): with a
+    Kerr spacetime it fails loudly instead of silently running another kernel."""
     c = Case("spheres_96x72_s1")
     with pytest.raises(rrt.RRTError) as e:
         gpu_render(gpu, c, 0.5, (0.0, 1.0, 0.0), flags=rrt.RRT_RENDER_WAVEFRONT)

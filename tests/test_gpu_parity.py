@@ -67,6 +67,8 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
             "nopixelproof": rrt.RRT_RENDER_NO_PIXEL_PROOF, "nosearch": rrt.RRT_RENDER_NO_SEARCH_TREE,
             "deepsample": rrt.RRT_RENDER_DEEP_SAMPLE, "noheavy": rrt.RRT_RENDER_NO_HEAVY,
             "heavy": rrt.RRT_RENDER_HEAVY}
+# the path pool kernel (RRT_RENDER_WAVEFRONT) exists for depth >= 2 only
+DEEP_VARIANTS = {"pathpool": rrt.RRT_RENDER_WAVEFRONT}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -74,6 +76,16 @@ VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_S
 def test_small_cases(gpu, name, variant):
     c = Case(name)
     rgb, cnt, draws, _ = render(gpu, c, flags=VARIANTS[variant])
+    print(variant, end=" ")
+    check(c, rgb, cnt, draws)
+
+
+@pytest.mark.parametrize("variant", sorted(DEEP_VARIANTS))
+@pytest.mark.parametrize("name", [n for n in SMALL if Case(n).cfg["max_ray_depth"] >= 2])
+def test_small_deep_cases(gpu, name, variant):
+    c = Case(name)
+    rgb, cnt, draws, _ = render(gpu, c, flags=DEEP_VARIANTS[variant])
+    assert "rrt_path_kernel" in gpu.stats().kernel.decode()
     print(variant, end=" ")
     check(c, rgb, cnt, draws)
 

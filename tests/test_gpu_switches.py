@@ -17,7 +17,10 @@ pytestmark = pytest.mark.gpu
 CASES = [
     ("spheres_96x72_s64_a16", {}, dict(adaptive=False), rrt.RRT_RENDER_NO_ADAPTIVE),
     ("spheres_96x72_s1", {}, dict(illum=0), rrt.RRT_RENDER_ILLUM(0)),
-    ("spheres_96x72_s8_l4", {}, dict(illum=1), rrt.RRT_RENDER_ILLUM(1)),
+    # (CBspheres' shadow rays all end on the light's own emitter mesh -- the reference drops the
+    # shadow ray's max_t -- so its direct light is zero: ILLUM 1 / 3 run on the lit bunny)
+    ("bunny_160x120_s16", {}, dict(illum=1), rrt.RRT_RENDER_ILLUM(1)),
+    ("bunny_160x120_s16", {"max_ray_depth": 3}, dict(illum=3), rrt.RRT_RENDER_ILLUM(3)),
     ("spheres_96x72_s8_l4", {"max_ray_depth": 2}, dict(illum=3), rrt.RRT_RENDER_ILLUM(3)),
     ("spheres_96x72_s8_l4", {"max_ray_depth": 1}, dict(illum=3), rrt.RRT_RENDER_ILLUM(3)),
     ("spheres_96x72_s8_l4", {}, dict(thin_lens=True), rrt.RRT_RENDER_THIN_LENS),

@@ -54,11 +54,13 @@ def test_illum0_is_normal_shading():
 
 def test_illum1_drops_only_the_emission():
     """ILLUM 1 at depth 1: direct lighting without the zero-bounce term, on the same draws.  A pixel
-    none of whose samples sees an emitter gets the default build's bits exactly; the others get less."""
-    c = Case("spheres_96x72_s8_l4")
+    none of whose samples sees an emitter gets the default build's bits exactly; the others get less.
+    (CBbunny: CBspheres' shadow rays all end on its light's emitter mesh, so its direct light is 0)"""
+    c = Case("bunny_160x120_s16")
     r2, n2, d2, _ = render(c, adaptive=False)
     r1, n1, d1, _ = render(c, adaptive=False, illum=1)
     assert np.array_equal(n1, n2) and np.array_equal(d1, d2)
+    assert float(r1.max()) > 0
     same = (r1.view(np.uint32) == r2.view(np.uint32)).all(-1)
     assert same.mean() > 0.8
     assert (r2[~same].sum(-1) >= r1[~same].sum(-1)).all()
@@ -67,9 +69,9 @@ def test_illum1_drops_only_the_emission():
 def test_illum3_keeps_only_bounces():
     """ILLUM 3: at_least_one_bounce_radiance alone, with the first hit's direct light zeroed (its
     draws still taken): darker than the default build on the same draws."""
-    c = Case("spheres_96x72_s8_l4")
-    r2, n2, d2, _ = render(c, adaptive=False, max_ray_depth=2)
-    r3, n3, d3, _ = render(c, adaptive=False, max_ray_depth=2, illum=3)
+    c = Case("bunny_160x120_s16")
+    r2, n2, d2, _ = render(c, adaptive=False, max_ray_depth=3)
+    r3, n3, d3, _ = render(c, adaptive=False, max_ray_depth=3, illum=3)
     assert np.array_equal(n2, n3)
     assert 0 < r3.sum() < r2.sum()
 

@@ -52,16 +52,24 @@ for step in "$@"; do
            run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0}
            run pmc_wait 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_wait -o run --output-format csv -- python3 tools/ab_kernels.py --rounds 1 ${AB_VARIANTS:-def:0:0} ;;
     hang)  # diagnostic build with the watchdog (RRT_WATCHDOG_MS): the round-3 profile-build hang case
-           run hang_b1 180 env RRT_LIB=tools/librrt_prof_wd.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
-           run hang_cfg3 180 env RRT_LIB=tools/librrt_prof_wd.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540 ;;
+           run hang_b1 180 env RRT_LIB=tools/librrt_prof.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
+           run hang_cfg3 180 env RRT_LIB=tools/librrt_prof.so RRT_WATCHDOG_MS=20000 python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540 ;;
     hang_nowd)  # the same diagnostic build without the watchdog (round 3's exact command shape)
-           run hang_b1_nowd 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
-           run hang_cfg3_nowd 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540
-           run hang_cfg3_full 60 env RRT_LIB=tools/librrt_prof_wd.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 2097152 ;;
+           run hang_b1_nowd 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
+           run hang_cfg3_nowd 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540
+           run hang_cfg3_full 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 2097152 ;;
     prof8) # kernel trace of every rank's tile set of the 8-way cfg3 split (batch vs heavy kernel per launch)
            run prof8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 ;;
     kerr)  run pytest_kerr 600 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 300 --timeout-method thread ;;
     cli)   run pytest_cli 600 python3 -u -m pytest tests/test_gpu_cli.py -x -q -s --timeout 300 --timeout-method thread ;;
+    phase8) # phase profiles of the slowest and the fastest rank's tile sets of the 8-way cfg3 split
+           RRT_LIB=tools/librrt_prof.so run ph8_r4 300 python3 tools/phase_profile.py --flags 0 --rank 4 8 &&
+           RRT_LIB=tools/librrt_prof.so run ph8_r0 300 python3 tools/phase_profile.py --flags 0 --rank 0 8 ;;
+    path)  # the path pool kernel (depth >= 2): its own parity tests, then every depth >= 2 golden in every variant
+           run pytest_path 300 python3 -u -m pytest tests/test_gpu_path.py -x -v -s --timeout 120 --timeout-method thread &&
+           run pytest_deep 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
+    pathprof) RRT_LIB=tools/librrt_prof.so run pathprof 300 python3 tools/path_profile.py --workload m3 ;;
+    ab8)   run ab8 900 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds ${AB_ROUNDS:-3} ${AB_WVARIANTS:-0 4096} ;;
     abw)   run abw 900 python3 tools/ab_workload.py --workload ${AB_WORKLOAD:-cfg5} --rounds ${AB_ROUNDS:-2} ${AB_WVARIANTS:-0 0:2048} ;;
     prof5) run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline ;;
     diag)  run diag 600 python3 tools/diag_clear.py --res 64 128 192 256 ;;
@@ -80,7 +88,7 @@ for step in "$@"; do
            run pmc_json_$W 60 python3 tools/pmc_valu.py gpurun_out/pmcv_$W gpurun_out/pmcf_$W gpurun_out/pmcw_$W --workload $W --kernel "$K" --out gpurun_out/r03_${W}_pmc.json ;;
     cropw) # the streak crop at 2..5 waves/SIMD (register budget vs spills) and its phase profile
            run cropw 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0:2 0:3 0:4 0:5 &&
-           RRT_LIB=tools/_var/librrt_prof.so run crop_phase 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
+           RRT_LIB=tools/librrt_prof.so run crop_phase 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
     cropd) # the streak crop without walks (diagnostic flags; results are not the reference's) and its counters
            run cropd 300 python3 tools/crop_probe.py --region 960 600 24 16 --flags 0 1073741824 268435456 536870912 65536 ;;
     crop)  run crop 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0 262144 ;;
@@ -92,16 +100,16 @@ for step in "$@"; do
            run pytest_heavy 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "baseline or noheavy or bunny_B or spheres_B" &&
            run abheavy 600 python3 tools/ab_workload.py --workload cfg3 --rounds 3 0 0:1048576 65536 196608 &&
            run profheavy 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profheavy -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --rounds 2 0 0:1048576 &&
-           RRT_LIB=tools/_var/librrt_prof.so run phase3h 300 python3 tools/phase_profile.py --flags 0 ;;
+           RRT_LIB=tools/librrt_prof.so run phase3h 300 python3 tools/phase_profile.py --flags 0 ;;
     profheavy) # per-kernel durations with and without the heavy path (cfg3)
            run profheavy 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profheavy -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --rounds 2 0 0:1048576 ;;
     phaseall) # phase profiles of cfg3 (frame + streak crop), cfg4 and cfg5 on the -DRRT_PROFILE=1 build (make prof)
-           RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
-           RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 &&
-           RRT_LIB=tools/_var/librrt_prof.so run phase4 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 &&
-           RRT_LIB=tools/_var/librrt_prof.so run phase5 600 python3 tools/phase_profile.py --workload cfg5 --flags 0 ;;
-    phase) RRT_LIB=tools/_var/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
-           RRT_LIB=tools/_var/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
+           RRT_LIB=tools/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
+           RRT_LIB=tools/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 &&
+           RRT_LIB=tools/librrt_prof.so run phase4 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 &&
+           RRT_LIB=tools/librrt_prof.so run phase5 600 python3 tools/phase_profile.py --workload cfg5 --flags 0 ;;
+    phase) RRT_LIB=tools/librrt_prof.so run phase3 300 python3 tools/phase_profile.py --flags 0 &&
+           RRT_LIB=tools/librrt_prof.so run phase_crop 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
     abdeep) run abdeep 900 python3 tools/ab_workload.py --workload m3 --rounds 2 0 2 4 0:16 0:131072 ;;
     deeptests) run pytest_deep 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "m2 or m3 or m4" ;;
     pmcall) # PMC of every workload's main kernel on this build, copied into profiles/ for the bench lines

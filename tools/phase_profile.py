@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--tiles", type=int, nargs="*", default=None, help="x y pairs of 32x32 tiles (default: all)")
     ap.add_argument("--region", type=int, nargs=4, default=None, help="x0 y0 w h: render only this region")
     ap.add_argument("--workload", default=None, help="a bench.py workload (cfg2..cfg5, m3) instead of a golden case")
+    ap.add_argument("--rank", type=int, nargs=2, default=None, metavar=("K", "N"),
+                    help="rank K's tile set of bench.py's N-way split (rrt_partition_tiles)")
     a = ap.parse_args()
     L = rrt.lib()
     L.rrt_prof_read.argtypes = [C.c_void_p]
@@ -58,6 +60,9 @@ def main():
     tiles = rrt.partition_tiles(frame_w, frame_h, 32, 0, 1)
     if a.tiles:
         tiles = np.array(a.tiles, np.uint32).reshape(-1, 2)
+    if a.rank:
+        tiles = rrt.partition_tiles(frame_w, frame_h, 32, a.rank[0], a.rank[1])
+        a.case = f"{a.case}_rank{a.rank[0]}of{a.rank[1]}"
     n = len(tiles) * 1024
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
