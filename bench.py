@@ -129,6 +129,9 @@ FP64_CYCLES_PER_WAVE_INST = 4.0
 N_SIMD = 1024
 
 
+PROFILE_ROUNDS = ("r04", "r03")  # profiles/ files searched, newest first (each must match the build)
+
+
 def find_profile(explicit, names, workload, kernel):
     """The first profiles/ JSON (or the explicit path) recorded for this workload, kernel and
     librrt.so build (rrt.build_id) -- numbers from another build are never attached to this line."""
@@ -305,10 +308,10 @@ def main():
     ap.add_argument("--cpu-row-stride", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--traffic", default=None,
                     help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for roofline.traffic; "
-                         "default profiles/r03_traffic_<workload>.json")
+                         "default profiles/r0N_traffic_<workload>.json, newest round first")
     ap.add_argument("--pmc", default=None,
                     help="PMC FP64 VALU counters per launch (tools/pmc_valu.py) for the fp64_valu roofline; "
-                         "default profiles/r03_<workload>_pmc.json")
+                         "default profiles/r0N_<workload>_pmc.json, newest round first")
     a = ap.parse_args()
 
     mode = check_world(a.gpus)
@@ -425,8 +428,8 @@ def main():
     loc_bytes = BYTES_AABB * xc4[0] + BYTES_PRIM * xc4[2] + BYTES_PLANE * xc4[3] + BYTES_PIXEL * pix_local
     ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
     main_kernel = kernel_name.split(" + ")[-1]
-    traffic = find_profile(a.traffic, [f"r03_traffic_{a.workload}.json"], a.workload, kernel_name)
-    pmc = find_profile(a.pmc, [f"r03_{a.workload}_pmc.json"], a.workload, main_kernel)
+    traffic = find_profile(a.traffic, [f"{r}_traffic_{a.workload}.json" for r in PROFILE_ROUNDS], a.workload, kernel_name)
+    pmc = find_profile(a.pmc, [f"{r}_{a.workload}_pmc.json" for r in PROFILE_ROUNDS], a.workload, main_kernel)
 
     verified = None
     if rank == 0:

@@ -1588,6 +1588,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     kp.heavy_grid = heavy_grid;
     kp.heavy_nw = (uint32_t)heavy_nw;
   }
+  // tail priority threshold (A/B: RRT_AB_PRIO_TICKS in the environment)
+  kp.prio_ticks = 50000u;
+  if (const char* pt = std::getenv("RRT_AB_PRIO_TICKS")) kp.prio_ticks = (uint32_t)std::strtoul(pt, nullptr, 10);
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
   HIPCHK(c, hipEventRecord(c->ev0[ring], stream));

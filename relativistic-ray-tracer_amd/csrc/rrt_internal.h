@@ -218,6 +218,9 @@ struct KParams {
   // the path pool kernel (rrt_path.hip, depth >= 2): each path's per-level terms of
   // at_least_one_bounce_radiance, [level][field][path] (RRT_PATH_FIELDS floats a level)
   float* path_stack;
+  // batch kernel: a wave whose oldest pixel has run this long (wall-clock ticks, 100 MHz) takes
+  // issue priority 2, four times as long priority 3 (rrt_sample.hip tail_prio)
+  uint32_t prio_ticks, prio_pad;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

@@ -364,7 +364,7 @@ struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128
 #define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
 #endif
 #ifndef RRT_PRIO_TICKS
-#define RRT_PRIO_TICKS 50000  // 0.5 ms of wall clock (100 MHz): a long-running pixel
+#define RRT_PRIO_TICKS 50000  // 0.5 ms of wall clock (100 MHz): a long-running pixel (KParams::prio_ticks)
 #endif
 
 // Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
@@ -703,8 +703,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     auto tail_prio = [&]() {
       if (!RRT_TAIL_PRIO) return;
       const uint64_t age = have ? wall_clock64() - t_claim : 0;
-      if (__ballot(age > 4 * RRT_PRIO_TICKS)) __builtin_amdgcn_s_setprio(3);
-      else if (__ballot(age > RRT_PRIO_TICKS)) __builtin_amdgcn_s_setprio(2);
+      if (__ballot(age > 4ull * kp.prio_ticks)) __builtin_amdgcn_s_setprio(3);
+      else if (__ballot(age > kp.prio_ticks)) __builtin_amdgcn_s_setprio(2);
       else __builtin_amdgcn_s_setprio(0);
     };
     tail_prio();

@@ -85,7 +85,7 @@ for step in "$@"; do
            run pmc_valu_$W 600 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmcv_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
            run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmcf_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
            run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmcw_$W -o run --output-format csv -- python3 bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline
-           run pmc_json_$W 60 python3 tools/pmc_valu.py gpurun_out/pmcv_$W gpurun_out/pmcf_$W gpurun_out/pmcw_$W --workload $W --kernel "$K" --out gpurun_out/r03_${W}_pmc.json ;;
+           run pmc_json_$W 60 python3 tools/pmc_valu.py gpurun_out/pmcv_$W gpurun_out/pmcf_$W gpurun_out/pmcw_$W --workload $W --kernel "$K" --out gpurun_out/${RTAG:-r04}_${W}_pmc.json ;;
     cropw) # the streak crop at 2..5 waves/SIMD (register budget vs spills) and its phase profile
            run cropw 300 python3 tools/crop_probe.py --region 960 600 24 16 --no-counters --flags 0:2 0:3 0:4 0:5 &&
            RRT_LIB=tools/librrt_prof.so run crop_phase 300 python3 tools/phase_profile.py --region 960 600 24 16 --flags 0 ;;
@@ -115,7 +115,7 @@ for step in "$@"; do
     pmcall) # PMC of every workload's main kernel on this build, copied into profiles/ for the bench lines
            for wk in "cfg3:rrt_batch_kernel<1, 4>" "cfg4:rrt_batch_kernel<2, 5>" "cfg2:rrt_batch_kernel<1, 4>" "m3:rrt_render_kernel<true, false, 0, ...>" "cfg5:rrt_batch_kernel<3, 3>"; do
              PMC_WORKLOAD=${wk%%:*} PMC_KERNEL=${wk#*:} bash tools/gpu_session.sh valu || exit $?
-             cp gpurun_out/r03_${wk%%:*}_pmc.json profiles/ ; done ;;
+             cp gpurun_out/${RTAG:-r04}_${wk%%:*}_pmc.json profiles/ ; done ;;
     profall) run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
              run prof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --workload cfg4 --steps 3 --warmup 1 --no-cpu-baseline &&
              run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 1 --warmup 1 --no-cpu-baseline &&
