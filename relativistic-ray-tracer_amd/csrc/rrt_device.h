@@ -592,15 +592,10 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
 // behind the result-identical skips -- filling *is on a hit.  Shared by the
 // Schwarzschild march below and the Kerr march (query_kerr).
 // any_rt: a shadow query chosen at run time (the path pool kernel's rays share one query call)
+// The walk of a segment that passed the skips (segment_query); cell: its start's grid cell or -1.
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, v3 e, Isect* is,
-                                              Counters& cn, bool any_rt = false) {
-  // e = o + d * max_t.  COUNT && kp.count_exec: count the work this path executes (grid / root
-  // skips, clean walk, plane tests in the query slot) instead of the reference's
-  const bool opt = !COUNT || kp.count_exec;
-  if (opt && segment_outside_root(kp, o, e)) return false;  // root test fails
-  const int cell = opt ? grid_cell(kp.grid, o) : -1;
-  if (cell_clear(kp.grid, cell, max_t)) return false;  // no primitive within reach
+__device__ __forceinline__ bool segment_walk(const KParams& kp, v3 o, v3 d, double max_t, v3 e, int cell,
+                                             Isect* is, Counters& cn, bool any_rt = false) {
   // oversized leaves with no primitive within reach of a short segment are not offered
   const uint64_t bmask = (kp.big_mask && cell >= 0 && max_t < kp.big_reach) ? (uint64_t)kp.big_mask[cell] : ~0ull;
   if (!COUNT && kp.diag) {  // diagnostics: skip all / interior-start / exterior-start walks
@@ -648,6 +643,17 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
     }
   }
   return true;
+}
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, v3 e, Isect* is,
+                                              Counters& cn, bool any_rt = false) {
+  // e = o + d * max_t.  COUNT && kp.count_exec: count the work this path executes (grid / root
+  // skips, clean walk, plane tests in the query slot) instead of the reference's
+  const bool opt = !COUNT || kp.count_exec;
+  if (opt && segment_outside_root(kp, o, e)) return false;  // root test fails
+  const int cell = opt ? grid_cell(kp.grid, o) : -1;
+  if (cell_clear(kp.grid, cell, max_t)) return false;  // no primitive within reach
+  return segment_walk<ANY, COUNT>(kp, o, d, max_t, e, cell, is, cn, any_rt);
 }
 
 // ------------------------------------------------------------------ kernel variants
@@ -971,6 +977,9 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
 #else
 #define RRT_QACC(v)
 #endif
+#ifndef RRT_QUERY_AHEAD
+#define RRT_QUERY_AHEAD 0  // 1: lanes skip ahead to their next walk (A/B; slower, profiles/r04_ab_query_ahead.txt)
+#endif
 #ifndef RRT_QUERY_ATTR  // a translation unit may force the query inline (rrt_path.hip)
 #define RRT_QUERY_ATTR __device__
 #endif
@@ -981,6 +990,43 @@ RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn
   RRT_T0(tq0);
   double max_t = 0.0;
   v3 e = o + vmul(d, max_t);  // the next segment's start (micro = Ray(o, d, max_t = 0), bvh.cpp:104)
+#if RRT_QUERY_AHEAD
+  // Lanes meet at walks, not at step indices: each lane advances its own march to its next
+  // segment that needs a walk (not captured, not skipped), then the wave's lanes walk together.
+  // Stepping in lock-step by index would make every lane wait, at each step, for the longest
+  // walk any lane has at that index.  Same steps and walks per lane, in the same order.
+  if (!COUNT) {
+    int j = 0;
+#pragma unroll 1
+    for (;;) {
+      bool walk = false;
+      int cell = -1;
+#pragma unroll 1
+      while (j < kp.hole.steps) {
+        RRT_T0(tm0);
+        v3 rel;
+        double rel2;
+        next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
+        RRT_ACC(t_micro, tm0);
+        ++j;
+        if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) break;  // captured: no hit
+        e = o + vmul(d, max_t);
+        if (segment_outside_root(kp, o, e)) continue;
+        cell = grid_cell(kp.grid, o);
+        if (cell_clear(kp.grid, cell, max_t)) continue;
+        walk = true;
+        break;
+      }
+      if (!walk) break;
+      if (segment_walk<ANY, false>(kp, o, d, max_t, e, cell, is, cn, any_rt)) {
+        RRT_QACC(tq0);
+        return true;
+      }
+    }
+    RRT_QACC(tq0);
+    return false;
+  }
+#endif
   for (int j = 0; j < kp.hole.steps; ++j) {
     RRT_T0(tm0);
     v3 rel;

@@ -9,7 +9,7 @@ WL=$1; PASSES=$2; shift 2
 for p in $(seq 1 "$PASSES"); do
   for name in "$@"; do
     lib=relativistic-ray-tracer_amd/librrt.so
-    [ "$name" != base ] && lib=tools/_var/librrt_$name.so
+    [ "$name" != base ] && lib=ab_var/librrt_$name.so
     RRT_LIB=$lib timeout -k 10 300 python3 tools/ab_workload.py --workload "$WL" --rounds 3 0 > gpurun_out/ab_${WL}_${name}_$p.log 2>&1
     rc=$?
     echo "$WL $name pass $p rc=$rc $(tail -1 gpurun_out/ab_${WL}_${name}_$p.log)" | tee -a gpurun_out/ab_libs.log

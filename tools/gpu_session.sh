@@ -58,6 +58,15 @@ for step in "$@"; do
            run hang_b1_nowd 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case bunny_B1_160x120_s16 --flags 2097152
            run hang_cfg3_nowd 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 0 --region 0 0 1920 540
            run hang_cfg3_full 60 env RRT_LIB=tools/librrt_prof.so python3 tools/phase_profile.py --case cfg3_bunny_1080p_s64 --flags 2097152 ;;
+    phase8all) # per-pixel time maps (gpurun_out/px_*.npz) of every rank's tile set of the 8-way cfg3 split
+           for k in 0 1 2 3 4 5 6 7; do
+             RRT_LIB=tools/librrt_prof.so run ph8_r$k 300 python3 tools/phase_profile.py --flags 0 --rank $k 8 || exit $?; done ;;
+    abq)   # A/B of two builds (in-tree vs ab_var/librrt_$ABQ_VAR.so): cfg3 bit-exact + frame time, then the 8-way split
+           run abq_exact 300 python3 tools/ab_kernels.py --rounds 3 def:0:0 &&
+           run abq_exact_var 300 env RRT_LIB=ab_var/librrt_${ABQ_VAR}.so python3 tools/ab_kernels.py --rounds 3 def:0:0 &&
+           bash tools/ab_libs.sh cfg3 2 base ${ABQ_VAR} &&
+           run abq_w8 300 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 &&
+           run abq_w8_var 300 env RRT_LIB=ab_var/librrt_${ABQ_VAR}.so python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 ;;
     prof8) # kernel trace of every rank's tile set of the 8-way cfg3 split (batch vs heavy kernel per launch)
            run prof8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 ;;
     kerr)  run pytest_kerr 600 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 300 --timeout-method thread ;;
