@@ -565,17 +565,22 @@ static inline void kerr_step(const hole_t* h, v3* q, v3* p, v3 dq1, v3 dp1, doub
   *q = vadd(*q, vmul(aq, c6));
   *p = vadd(*p, vmul(ap, c6));
 }
-/* one march step: 0 = stepped, 1 = escaped (outgoing beyond r_esc); *swept += polar angle */
-static inline int kerr_advance(const hole_t* h, v3* q, v3* p, double* swept) {
+/* one march step: 0 = stepped, 1 = escaped (outgoing beyond r_esc); *swept += polar angle.
+ * st: step stretch (1 for the march; the coarse march of the Kerr occlusion proof's sweep, tests/
+ * kerr_proof_sim.py, takes st > 1: h = st * dtheta * r / |dq/dl|) */
+static inline int kerr_advance_st(const hole_t* h, v3* q, v3* p, double* swept, double st) {
   v3 dq1, dp1;
   double r;
   kerr_rhs(h, *q, *p, &dq1, &dp1, &r);
   const double rho2 = vnorm2(*q);
   if (rho2 > h->r_esc2 && vdot(*q, dq1) > 0.0) return 1;
-  const double hh = (h->dt * r) / vnorm(dq1);
+  const double hh = ((h->dt * r) * st) / vnorm(dq1);
   *swept += (hh * vnorm(vcross(*q, dq1))) / rho2;
   kerr_step(h, q, p, dq1, dp1, hh);
   return 0;
+}
+static inline int kerr_advance(const hole_t* h, v3* q, v3* p, double* swept) {
+  return kerr_advance_st(h, q, p, swept, 1.0);  /* (dt r) * 1 = dt r exactly */
 }
 
 typedef struct {
@@ -1107,7 +1112,8 @@ int ro_render(const ro_scene* s, const ro_camera* cam, const ro_params* p, uint3
 }
 
 /* ------------------------------------------------------------------ KAT entry points */
-int ro_kerr_chain(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame) {
+int ro_kerr_chain_st(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame,
+                     double st, double* extra) {
   hole_t h; hole_init_kerr(&h, bh, bh[3], bh[4], bh[5], bh + 6);
   if (frame) {
     frame[0] = h.ex.x; frame[1] = h.ex.y; frame[2] = h.ex.z; frame[3] = h.ey.x; frame[4] = h.ey.y;
@@ -1119,7 +1125,7 @@ int ro_kerr_chain(const double* bh, const double* o, const double* d, double* ou
   int rows = 0;
   double swept = 0.0;
   while (rows < max_rows) {  /* physics checks: no escape cutoff, no sweep or step budget */
-    kerr_advance(&h, &q, &p, &swept);
+    kerr_advance_st(&h, &q, &p, &swept, st);
     const int cap = kerr_r2(&h, q) <= rh2;
     const v3 b = kerr_world(&h, q);
     v3 sd = vsub(b, a);
@@ -1128,12 +1134,31 @@ int ro_kerr_chain(const double* bh, const double* o, const double* d, double* ou
     double* r = out + 14 * rows++;
     r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = sd.x; r[4] = sd.y; r[5] = sd.z; r[6] = mt; r[7] = cap;
     r[8] = q.x; r[9] = q.y; r[10] = q.z; r[11] = p.x; r[12] = p.y; r[13] = p.z;
+    if (extra) {  /* the swept polar angle after the step and the segment's end point */
+      double* x = extra + 4 * (rows - 1);
+      x[0] = swept; x[1] = b.x; x[2] = b.y; x[3] = b.z;
+    }
     if (cap) break;
     a = b;
   }
   return rows;
 }
 
+int ro_kerr_chain(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame) {
+  return ro_kerr_chain_st(bh, o, d, out, max_rows, frame, 1.0, NULL);
+}
+/* The shadow query of the ray (o, d) -- BVHAccel::intersect's boolean (bvh.cpp:103-113) -- with the
+ * spacetime of params p (Schwarzschild stepper or the Kerr march).  Sweep checks of the proofs. */
+int ro_shadow_query(const ro_scene* s, const ro_params* p, const double* o, const double* d) {
+  rng_t g; memset(&g, 0, sizeof(g));
+  qctx q; q.s = s; q.g = &g;
+  if (p->bh_kind == 1) {
+    hole_init_kerr(&q.hole, p->bh_center, p->bh_radius, p->bh_dtheta, p->bh_spin, p->bh_axis);
+    kerr_set_escape(&q.hole, s->nodes[0].mn, s->nodes[0].mx);
+  } else hole_init(&q.hole, p->bh_center, p->bh_radius, p->bh_dtheta);
+  isect_t is; memset(&is, 0, sizeof(is));
+  return bvh_intersect(&q, V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), &is);
+}
 int ro_micro_chain(const double* bh, const double* o, const double* d, double* out, int max_rows) {
   hole_t h; hole_init(&h, bh, bh[3], bh[4]);
   ray_t m; m.o = V(o[0], o[1], o[2]); m.d = V(d[0], d[1], d[2]); m.min_t = 0; m.max_t = 0;

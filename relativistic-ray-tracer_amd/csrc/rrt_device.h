@@ -780,14 +780,15 @@ __device__ __forceinline__ void kerr_init(const DHole& h, v3 o, v3 d, v3& q, v3&
 // One march step: the first RK4 stage at (q, p); escape test (outgoing beyond r_esc: returns
 // true); h = delta_theta * r / |dq/dl| (the path advances delta_theta * r); the polar angle
 // swept; then the classical RK4 update.
+// st: step stretch (1: the march; the occlusion proof's coarse march takes kp.kproof.stretch)
 template <class A>
-__device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, double& swept, A& ar) {
+__device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, double& swept, A& ar, double st = 1.0) {
   v3 dq1, dp1;
   double r, rr;
   kerr_rhs(h, q, p, dq1, dp1, r, ar);
   const double rho2 = norm2(q);
   if (rho2 > h.r_esc2 && dot(q, dq1) > 0.0) return true;  // outgoing beyond the scene
-  const double hh = ar.dv(h.dt * r, ar.sq(norm2(dq1)));
+  const double hh = ar.dv((h.dt * r) * st, ar.sq(norm2(dq1)));  // (dt r) * 1 = dt r exactly
   swept += ar.dv(hh * ar.sq(norm2(cross(q, dq1))), rho2);  // polar angle of this step
   const double half = 0.5 * hh;
   // stages 2-4 folded into running sums as they come: ((k1 + 2 k2) + 2 k3) + k4, the same
@@ -811,8 +812,11 @@ __device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, doubl
 // outer horizon.  Steps are sized by distance (accurate for radial motion too), so the sweep is
 // budgeted by angle, not by count (at most kerr_max_steps), and a photon moving outward beyond
 // every primitive (|q|^2 > r_esc2 >= (4M)^2, outside all photon orbits) has escaped: no hit.
+__device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d);
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
+  // shadow rays: the occlusion proof first (never in the reference-work counts)
+  if (ANY && kp.kproof.on && !(COUNT && !kp.count_exec) && kerr_occluded_proof(kp, o, d)) return true;
   const DHole& h = kp.hole;
   v3 q, p;
   kerr_init(h, o, d, q, p);
@@ -903,6 +907,104 @@ __device__ __noinline__ int occ_exit_call(const KParams& kp, v3 a, v3 b, double 
 __device__ __forceinline__ bool occ_inside(const DShadowProof& sp, v3 b) {
   return b.x >= sp.in_lo[0] && b.x <= sp.in_hi[0] && b.y >= sp.in_lo[1] && b.y <= sp.in_hi[1] && b.z >= sp.in_lo[2] &&
          b.z <= sp.in_hi[2];
+}
+// Kerr shadow rays ("Kerr occlusion proof").  A shadow query is true iff some
+// segment of the march before the capture hits a primitive; from inside a closed room most end on
+// a wall after 20-60 RK4 steps, each step four Hamiltonian evaluations plus a walk.  The proof
+// marches the same Hamiltonian with steps kp.kproof.stretch times longer and accepts "occluded"
+// when one of its chords crosses a wall piece (build_occluders: kp.occ's triangles, coplanar pairs
+// merged into convex quads, kp.kproof.quad) with margin delta:
+// end points more than delta on either side of the plane, the crossing point inside every edge by
+// occ_face's mq.  The exact march's chords stay within delta of the coarse chords while the coarse
+// march keeps sqrt(r_near2) from the hole (tools/kerr_proof_sweep.py: the largest deviation seen
+// over the envelope rrt_host.cpp allows is under a third of delta), so they cross that triangle
+// too, uncaptured (the coarse path, and so the exact one, stays far outside the horizon) and
+// within the exact march's budget (max_steps coarse steps, swept angle below swept_max); the
+// triangle test accepts and the leaf boxes on the way contain the crossing, so the query is true.
+// Anything else -- near the hole, the ray leaving the room, an operand outside the fast cores'
+// range, the budget -- is no proof: the exact march runs.
+// occ_face / occ_exit on the Kerr proof's wall pieces (DOccQuad: a convex quad or a triangle)
+__device__ __forceinline__ bool occ_face_quad(const DKerrProof& kq, int f, v3 a, v3 b, double m) {
+#pragma clang fp contract(fast)
+#pragma unroll 1
+  for (uint32_t i = 0; i < kq.nq[f]; ++i) {
+    const DOccQuad& t = kq.quad[f][i];
+    const double da = t.n[0] * a.x + t.n[1] * a.y + t.n[2] * a.z - t.d;
+    const double db = t.n[0] * b.x + t.n[1] * b.y + t.n[2] * b.z - t.d;
+    if (!((da > m && db < -m) || (da < -m && db > m))) continue;
+    const double tq = da / (da - db);
+    const v3 q = V(a.x + (b.x - a.x) * tq, a.y + (b.y - a.y) * tq, a.z + (b.z - a.z) * tq);
+    const double mq = m * (2.0 + (fabs(b.x - a.x) + fabs(b.y - a.y) + fabs(b.z - a.z)) / fabs(da - db));
+    bool in = true;
+    for (int k = 0; k < 4; ++k) in = in && t.en[k][0] * q.x + t.en[k][1] * q.y + t.en[k][2] * q.z - t.eo[k] >= mq;
+    if (in) return true;
+  }
+  return false;
+}
+__device__ __forceinline__ int occ_exit_quad(const KParams& kp, v3 a, v3 b, double m) {
+  const DShadowProof& sp = kp.occ;
+  bool out = false;
+#pragma unroll 1
+  for (int f = 0; f < 6; ++f) {
+    const int k = f < 3 ? f : f - 3;
+    const double ak = k == 0 ? a.x : k == 1 ? a.y : a.z, bk = k == 0 ? b.x : k == 1 ? b.y : b.z;
+    const bool past = f < 3 ? !(bk >= sp.in_lo[k] && ak >= sp.in_lo[k]) : !(bk <= sp.in_hi[k] && ak <= sp.in_hi[k]);
+    if (past && occ_face_quad(kp.kproof, f, a, b, m)) return 1;
+    out = out || !(f < 3 ? bk >= kp.miss.lo[k] : bk <= kp.miss.hi[k]);  // NaN: out
+  }
+  return out ? -1 : 0;
+}
+__device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d) {
+  const DHole& h = kp.hole;
+  const DKerrProof& kq = kp.kproof;
+  {  // a ray whose straight line leaves the room through a face without wall pieces (the open side
+     // of a Cornell box) almost never ends on a wall: spare it the coarse march
+    double te = 1e300;
+    int fe = -1;
+    for (int k = 0; k < 3; ++k) {
+      const double dk = k == 0 ? d.x : k == 1 ? d.y : d.z, ok = k == 0 ? o.x : k == 1 ? o.y : o.z;
+      if (dk == 0.0) continue;
+      const double t = ((dk > 0.0 ? kp.miss.hi[k] : kp.miss.lo[k]) - ok) / dk;
+      if (t < te) { te = t; fe = dk > 0.0 ? k + 3 : k; }
+    }
+    if (fe >= 0 && kq.nq[fe] == 0) return false;
+  }
+  v3 q, p;
+  kerr_init(h, o, d, q, p);
+  if (!(norm2(q) > kq.r_near2)) return false;  // starting near the hole
+  const v3 c = ld3(h.c);
+  v3 a = o, a0 = o;  // the chord's start, and the previous chord's
+  bool a_in = occ_inside(kp.occ, a);
+  double swept = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < kq.max_steps; ++j) {
+    KArith<true> ar;
+    const bool escaped = kerr_advance(h, q, p, swept, ar, kq.stretch);
+    if (!ar.ok || escaped || !(swept < kq.swept_max) || !(norm2(q) > kq.r_near2)) return false;
+    const v3 b = kerr_world(h, q);
+    {  // the chord keeps sqrt(r_near2) from the hole too
+      const v3 u = b - a, w = c - a;
+      const double uu = norm2(u), t = uu > 0.0 ? fmin(fmax(dot(u, w) / uu, 0.0), 1.0) : 0.0;
+      if (!(norm2(w - vmul(u, t)) > kq.r_near2)) return false;
+    }
+    const bool b_in = occ_inside(kp.occ, b);
+    if (!b_in || !a_in) {
+      int res = occ_exit_quad(kp, a, b, kq.delta);
+      if (res <= 0 && j > 0) {
+        // a wall crossed across two chords (one of their common point's sides within delta of the
+        // plane): the chord a0 -> b, with the margin grown by a's distance from it
+        const v3 u = b - a0, w = a - a0;
+        const double uu = norm2(u), uw = dot(u, w);
+        const double beta = sqrt(fmax(norm2(w) - uw * uw / uu, 0.0)) * (1.0 + 1e-6);
+        if (uu > 0.0 && occ_exit_quad(kp, a0, b, kq.delta + beta) > 0) res = 1;
+      }
+      if (res) return res > 0;
+    }
+    a_in = b_in;
+    a0 = a;
+    a = b;
+  }
+  return false;
 }
 // The whole march by the recurrence, step 0 included: the ray (o, d) is the state of a step from
 // the point A = o itself (|A - c| = 1 / u, so v_prev = rho u, E_prev = x, s_prev chosen so the

@@ -48,6 +48,17 @@ constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_
 // Heavy pixels (rrt_sample.hip heavy_pixel_block): rays passing within RRT_HEAVY_NEAR r_s of the hole (or straddling
 // its capture boundary) make a pixel heavy (profiles/r03_heavy_ab.md)
 #define RRT_HEAVY_NEAR 1.2
+// Kerr occlusion proof (rrt_device.h kerr_occluded_proof): coarse steps RRT_KPROOF_STRETCH times the
+// march's, no proof within RRT_KPROOF_NEAR_M M of the hole, crossing margin RRT_KPROOF_DELTA_M M;
+// on for holes with delta_theta in [DT_MIN, DT_MAX], a/M <= SPIN_MAX and every root-box corner
+// within REACH_M M -- the envelope tools/kerr_proof_sweep.py swept (tests/test_kerr_proof.py)
+#define RRT_KPROOF_STRETCH 4.0
+#define RRT_KPROOF_NEAR_M 6.0
+#define RRT_KPROOF_DELTA_M 0.25
+#define RRT_KPROOF_DT_MIN 0.02
+#define RRT_KPROOF_DT_MAX 0.1
+#define RRT_KPROOF_SPIN_MAX 0.99
+#define RRT_KPROOF_REACH_M 40.0
 
 struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
@@ -165,6 +176,8 @@ struct rrt_ctx {
   uint64_t free_big_mask = ~0ull;   // oversized leaves the search-tree walk still tests from its list
   DNode* d_free = nullptr;
   DShadowProof occ{};               // build_occluders (the root box's face triangles)
+  DOccQuad occ_quad[6][RRT_OCC_PER_FACE]{};  // the same triangles, coplanar pairs merged (Kerr proof)
+  uint32_t occ_nq[6]{};
   uint32_t* d_big_mask = nullptr;
   uint64_t device_bytes = 0;
   // per-launch workspace
@@ -426,6 +439,7 @@ static bool grid_mark_leaf(const rrt_ctx* c, const double g0[3], double h, const
 static void build_occluders(rrt_ctx* c) {
   DShadowProof& o = c->occ;
   o = DShadowProof{};
+  std::memset(c->occ_nq, 0, sizeof(c->occ_nq));
   if (c->nodes.empty()) return;
   const Box& rb = c->nodes[0].bb;
   const double lo[3] = {rb.mn.x, rb.mn.y, rb.mn.z}, hi[3] = {rb.mx.x, rb.mx.y, rb.mx.z};
@@ -433,7 +447,7 @@ static void build_occluders(rrt_ctx* c) {
   for (int k = 0; k < 3; ++k) sc = std::max(sc, hi[k] - lo[k]);
   if (!(sc > 0.0) || !std::isfinite(sc)) return;
   const double tol = 1e-2 * sc;
-  struct Cand { double area, w; DOccluder t; };
+  struct Cand { double area, w; DOccluder t; V3 v[3]; };
   std::vector<Cand> cand[6];
   for (const Prim& p : c->prims) {
     if (p.kind != RRT_OBJ_MESH) continue;
@@ -472,7 +486,7 @@ static void build_occluders(rrt_ctx* c) {
         const V3 v = q[(i + 2) % 3];
         ok = t.en[i][0] * v.x + t.en[i][1] * v.y + t.en[i][2] * v.z - t.eo[i] > 0.0;
       }
-      if (ok) cand[f].push_back({0.5 * nl, w, t});
+      if (ok) cand[f].push_back({0.5 * nl, w, t, {q[0], q[1], q[2]}});
     }
   }
   for (int f = 0; f < 6; ++f) {
@@ -484,6 +498,58 @@ static void build_occluders(rrt_ctx* c) {
       o.tri[f][i] = cand[f][i].t;
       o.w[f] = std::max(o.w[f], cand[f][i].w);
     }
+    // The Kerr proof's wall pieces: two kept triangles that share an edge (vertices within 1e-9 of
+    // the box's extent), lie in one plane and form a convex quad are one piece -- the crossing may
+    // then land anywhere in the quad, not only inside one triangle -- else the triangle alone.
+    // (The reference tests both triangles; a crossing on the shared edge itself is accepted by one
+    // of them up to the rounding of triangle.cpp's barycentric signs there.)
+    bool used[RRT_OCC_PER_FACE] = {};
+    uint32_t nq = 0;
+    auto edge_of = [](int a, int b) { return ((a + 1) % 3 == b) ? a : b; };  // edge k: q[k] -> q[k + 1]
+    for (uint32_t i = 0; i < keep; ++i) {
+      if (used[i]) continue;
+      const Cand& A = cand[f][i];
+      DOccQuad qd{};
+      for (int k = 0; k < 3; ++k) qd.n[k] = A.t.n[k];
+      qd.d = A.t.d;
+      int ne = 0;
+      for (uint32_t j = i + 1; j < keep && !ne; ++j) {
+        if (used[j]) continue;
+        const Cand& B = cand[f][j];
+        int sa[2], sb[2], ns = 0;
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) {
+            const double dd = std::max(std::fabs(A.v[a].x - B.v[b].x),
+                                       std::max(std::fabs(A.v[a].y - B.v[b].y), std::fabs(A.v[a].z - B.v[b].z)));
+            if (dd <= 1e-9 * sc && ns < 2) { sa[ns] = a; sb[ns] = b; ++ns; }
+          }
+        if (ns != 2) continue;
+        const double cosn = A.t.n[0] * B.t.n[0] + A.t.n[1] * B.t.n[1] + A.t.n[2] * B.t.n[2];
+        if (!(cosn >= 1.0 - 1e-12) || !(std::fabs(A.t.d - B.t.d) <= 1e-9 * sc)) continue;
+        const int ka = edge_of(sa[0], sa[1]), kb = edge_of(sb[0], sb[1]);
+        const V3 fa = A.v[3 - sa[0] - sa[1]], fb = B.v[3 - sb[0] - sb[1]];  // the far vertices
+        bool convex = true;
+        for (int k = 0; k < 3 && convex; ++k) {
+          if (k != ka) convex = A.t.en[k][0] * fb.x + A.t.en[k][1] * fb.y + A.t.en[k][2] * fb.z - A.t.eo[k] > 0.0;
+          if (convex && k != kb)
+            convex = B.t.en[k][0] * fa.x + B.t.en[k][1] * fa.y + B.t.en[k][2] * fa.z - B.t.eo[k] > 0.0;
+        }
+        if (!convex) continue;
+        for (int k = 0; k < 3; ++k) {
+          if (k != ka) { for (int x = 0; x < 3; ++x) qd.en[ne][x] = A.t.en[k][x]; qd.eo[ne++] = A.t.eo[k]; }
+          if (k != kb) { for (int x = 0; x < 3; ++x) qd.en[ne][x] = B.t.en[k][x]; qd.eo[ne++] = B.t.eo[k]; }
+        }
+        used[j] = true;
+      }
+      if (!ne) {  // the triangle alone: its three edges, the first repeated
+        for (int k = 0; k < 4; ++k) {
+          for (int x = 0; x < 3; ++x) qd.en[k][x] = A.t.en[k % 3][x];
+          qd.eo[k] = A.t.eo[k % 3];
+        }
+      }
+      c->occ_quad[f][nq++] = qd;
+    }
+    c->occ_nq[f] = nq;
   }
 }
 
@@ -1298,6 +1364,30 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // the point-light scenes' builds carry no proof (rrt_sample.hip RRT_OCC_TAG); off for them in
     // every kernel, so the counting passes count what their batch kernel executes
     kp.occ.on = (proofs_valid && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
+    // Kerr shadow rays (rrt_device.h kerr_occluded_proof): the same face triangles
+    // against a coarse march, inside the envelope its margin was swept over
+    // (tools/kerr_proof_sweep.py -> profiles/r04_kerr_proof_sweep.json)
+    DKerrProof& kq = kp.kproof;
+    kq = DKerrProof{};
+    const DHole& h = kp.hole;
+    const bool kenv = h.kind == RRT_METRIC_KERR && any && fin && h.m > 0.0 && h.dt >= RRT_KPROOF_DT_MIN &&
+                      h.dt <= RRT_KPROOF_DT_MAX && h.a <= RRT_KPROOF_SPIN_MAX * h.m &&
+                      h.r_esc2 <= (RRT_KPROOF_REACH_M * h.m) * (RRT_KPROOF_REACH_M * h.m);
+    if (kenv && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) {
+      kq.stretch = RRT_KPROOF_STRETCH;
+      kq.r_near2 = (RRT_KPROOF_NEAR_M * h.m) * (RRT_KPROOF_NEAR_M * h.m);
+      kq.delta = RRT_KPROOF_DELTA_M * h.m;
+      kq.swept_max = 2.0 * M_PI - 0.5;
+      // the exact march takes about stretch steps per coarse step: a quarter to spare
+      kq.max_steps = (int32_t)((h.kerr_max_steps - 2) / (1.25 * kq.stretch));
+      kq.on = 1u;
+      std::memcpy(kq.quad, c->occ_quad, sizeof(kq.quad));
+      std::memcpy(kq.nq, c->occ_nq, sizeof(kq.nq));
+      for (int k = 0; k < 3; ++k) {  // trigger box: shrunk past every kept triangle by 2 delta
+        kp.occ.in_lo[k] = kp.miss.lo[k] + kp.occ.w[k] + 2.0 * kq.delta;
+        kp.occ.in_hi[k] = kp.miss.hi[k] - kp.occ.w[k + 3] - 2.0 * kq.delta;
+      }
+    }
   }
   kp.ns_aa = p->ns_aa; kp.max_ray_depth = p->max_ray_depth; kp.ns_area_light = p->ns_area_light;
   kp.samples_per_batch = p->samples_per_batch; kp.max_tolerance = p->max_tolerance;

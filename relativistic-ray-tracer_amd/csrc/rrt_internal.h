@@ -131,6 +131,23 @@ struct DShadowProof {
   uint32_t on, pad;
 };
 
+// Kerr shadow-ray occlusion proof (rrt_device.h kerr_occluded_proof): a coarse march
+// (steps stretch x delta_theta x r) whose chords the exact march's stay within delta of
+// A wall piece of the Kerr proof: an occluder triangle, or two coplanar ones of the same face that
+// share an edge and form a convex quad (a Cornell-box wall), as one convex polygon: plane (normal
+// toward the box's inside) and four inward in-plane edge normals (a triangle repeats one edge).
+struct DOccQuad { double n[3], d, en[4][3], eo[4]; };
+struct DKerrProof {
+  DOccQuad quad[6][RRT_OCC_PER_FACE];  // per root-box face (rrt_host.cpp build_occluders)
+  uint32_t nq[6];
+  double stretch;     // coarse step length over the exact march's
+  double r_near2;     // no proof once the coarse march comes within sqrt(r_near2) of the hole
+  double delta;       // crossing margin (tools/kerr_proof_sweep.py: >= 3x the largest deviation seen)
+  double swept_max;   // the coarse march's swept polar angle stays below it (the exact budget: 2 pi)
+  int32_t max_steps;  // coarse steps (so the exact march's step budget reaches the crossing)
+  uint32_t on;
+};
+
 #define RRT_MAX_QUEUES 8
 #define RRT_QUEUE_STRIDE 16  // counters 64 B apart
 
@@ -221,6 +238,7 @@ struct KParams {
   // batch kernel: a wave whose oldest pixel has run this long (wall-clock ticks, 100 MHz) takes
   // issue priority 2, four times as long priority 3 (rrt_sample.hip tail_prio)
   uint32_t prio_ticks, prio_pad;
+  DKerrProof kproof;      // Kerr builds: the shadow rays' occlusion proof (kp.occ's face triangles)
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

@@ -1,0 +1,185 @@
+"""Mirror of the Kerr shadow-ray occlusion proof (relativistic-ray-tracer_amd/csrc/rrt_device.h
+kerr_occluded_proof, constants from rrt_host.cpp RRT_KPROOF_*), one ray at a time, on the CPU
+restatement's coarse march (oracle/restate ro_kerr_chain_st: the same Hamiltonian, RK4 and step
+rule as the device's, steps `stretch` times longer).
+
+TEST INFRASTRUCTURE ONLY (tests/test_kerr_proof.py, tools/kerr_proof_sweep.py): the product runs the
+HIP version.
+
+The proof accepts "occluded" when a chord of the coarse march crosses one of the root box's wall
+triangles (the shadow proof's occluder table, tests/shadow_proof_sim.py) with margin delta, while the
+march stays sqrt(r_near2) from the hole and within the exact march's budget.  Its soundness rests on
+the exact march's chords staying within delta of the coarse ones: `deviation` measures that.
+"""
+import numpy as np
+
+import oracle_lib as O
+from shadow_proof_sim import _inside
+
+STRETCH = 4.0    # RRT_KPROOF_STRETCH
+NEAR_M = 6.0     # RRT_KPROOF_NEAR_M
+DELTA_M = 0.25   # RRT_KPROOF_DELTA_M
+DT_MIN, DT_MAX, SPIN_MAX, REACH_M = 0.02, 0.1, 0.99, 40.0
+
+
+def steps_of(dt):
+    j = 0
+    while j * dt < 2 * np.pi:
+        j += 1
+    return j
+
+
+def constants(bh, lo, hi, w):
+    """bh = (cx, cy, cz, r_s, dtheta); the proof's constants and trigger box as rrt_host.cpp sets them
+    (None outside the envelope)."""
+    c = np.array(bh[:3], np.float64)
+    m = 0.5 * float(bh[3])
+    dt = float(bh[4])
+    e = np.maximum(np.abs(lo - c), np.abs(hi - c))
+    r_esc2 = max(float((e * e).sum()), (4.0 * m) ** 2)
+    K = dict(c=c, m=m, dt=dt, lo=lo, hi=hi, stretch=STRETCH, r_near2=(NEAR_M * m) ** 2, delta=DELTA_M * m,
+             swept_max=2.0 * np.pi - 0.5, max_steps=int((4 * steps_of(dt) - 2) / (1.25 * STRETCH)), r_esc2=r_esc2)
+    K["box"] = (lo + w[:3] + 2.0 * K["delta"], hi - w[3:] - 2.0 * K["delta"])
+    K["in_envelope"] = DT_MIN <= dt <= DT_MAX and r_esc2 <= (REACH_M * m) ** 2
+    return K
+
+
+def quads(T, faces, lo, hi):
+    """rrt_host.cpp build_occluders' wall pieces: per face, coplanar kept triangles sharing an edge
+    and forming a convex quad merged; [(n, d, en [4,3], eo [4])]."""
+    sc = float(np.max(hi - lo))
+    out = []
+    for tris in faces:
+        used = [False] * len(tris)
+        pieces = []
+        for i, (n, d, en, eo, ti) in enumerate(tris):
+            if used[i]:
+                continue
+            A = np.stack([T[ti, 0], T[ti, 0] + (T[ti, 1] - T[ti, 0]), T[ti, 0] + (T[ti, 2] - T[ti, 0])])
+            piece = None
+            for j in range(i + 1, len(tris)):
+                if used[j] or piece is not None:
+                    continue
+                n2, d2, en2, eo2, tj = tris[j]
+                B = np.stack([T[tj, 0], T[tj, 0] + (T[tj, 1] - T[tj, 0]), T[tj, 0] + (T[tj, 2] - T[tj, 0])])
+                sh = [(a, b) for a in range(3) for b in range(3) if np.abs(A[a] - B[b]).max() <= 1e-9 * sc][:2]
+                if len(sh) != 2 or not n @ n2 >= 1 - 1e-12 or not abs(d - d2) <= 1e-9 * sc:
+                    continue
+                (a0, b0), (a1, b1) = sh
+                ka = a0 if (a0 + 1) % 3 == a1 else a1
+                kb = b0 if (b0 + 1) % 3 == b1 else b1
+                fa, fb = A[3 - a0 - a1], B[3 - b0 - b1]
+                if not all(en[k] @ fb - eo[k] > 0 for k in range(3) if k != ka):
+                    continue
+                if not all(en2[k] @ fa - eo2[k] > 0 for k in range(3) if k != kb):
+                    continue
+                E, O_ = [], []
+                for k in range(3):
+                    if k != ka:
+                        E.append(en[k]); O_.append(eo[k])
+                    if k != kb:
+                        E.append(en2[k]); O_.append(eo2[k])
+                piece = (n, d, np.array(E), np.array(O_))
+                used[j] = True
+            if piece is None:
+                piece = (n, d, np.array([en[k % 3] for k in range(4)]), np.array([eo[k % 3] for k in range(4)]))
+            pieces.append(piece)
+        out.append(pieces)
+    return out
+
+
+def _face_quad(pieces, a, b, m):
+    for n, d, en, eo in pieces:
+        da = n @ a - d
+        db = n @ b - d
+        if not ((da > m and db < -m) or (da < -m and db > m)):
+            continue
+        q = a + (b - a) * (da / (da - db))
+        mq = m * (2.0 + np.abs(b - a).sum() / abs(da - db))
+        if all(en[k] @ q - eo[k] >= mq for k in range(4)):
+            return True
+    return False
+
+
+def _exit_quad(pieces, box, lo, hi, a, b, m):
+    out = False
+    for f in range(6):
+        k = f % 3
+        past = not (b[k] >= box[0][k] and a[k] >= box[0][k]) if f < 3 else not (b[k] <= box[1][k] and a[k] <= box[1][k])
+        if past and _face_quad(pieces[f], a, b, m):
+            return 1
+        out = out or not (b[k] >= lo[k] if f < 3 else b[k] <= hi[k])
+    return -1 if out else 0
+
+
+def run(K, pieces, bh, spin, axis, o, d):
+    """kerr_occluded_proof for the ray (o, d): (proven, chain rows, chain extra).  pieces: quads()."""
+    o = np.asarray(o, np.float64)
+    d = np.asarray(d, np.float64)
+    te, fe = np.inf, -1
+    for k in range(3):  # the open-side gate
+        if d[k] == 0.0:
+            continue
+        t = ((K["hi"][k] if d[k] > 0 else K["lo"][k]) - o[k]) / d[k]
+        if t < te:
+            te, fe = t, (k + 3 if d[k] > 0 else k)
+    if fe >= 0 and len(pieces[fe]) == 0:
+        return False, np.zeros((0, 14)), np.zeros((0, 4))
+    rows, extra = O.kerr_chain_st(bh, spin, axis, o, d, K["stretch"], max_rows=K["max_steps"])
+    if not (o - K["c"]) @ (o - K["c"]) > K["r_near2"]:  # starting near the hole (|q| = |o - c|)
+        return False, rows[:0], extra[:0]
+    a = a0 = o
+    a_in = _inside(K["box"], a)
+    for j in range(len(rows)):
+        q = rows[j, 8:11]
+        swept, b = extra[j, 0], extra[j, 1:4]
+        # escape (outgoing beyond r_esc) needs a start outside the root box: occ_exit has ended the
+        # march before that
+        if not swept < K["swept_max"] or not q @ q > K["r_near2"]:
+            return False, rows[:j + 1], extra[:j + 1]
+        u, wv = b - a, K["c"] - a
+        uu = u @ u
+        t = min(max((u @ wv) / uu, 0.0), 1.0) if uu > 0 else 0.0
+        if not (wv - u * t) @ (wv - u * t) > K["r_near2"]:  # the chord keeps r_near from the hole
+            return False, rows[:j + 1], extra[:j + 1]
+        b_in = _inside(K["box"], b)
+        if not b_in or not a_in:
+            res = _exit_quad(pieces, K["box"], K["lo"], K["hi"], a, b, K["delta"])
+            if res <= 0 and j > 0:  # across two chords: a0 -> b, the margin grown by a's distance
+                u, w = b - a0, a - a0
+                uu = u @ u
+                beta = np.sqrt(max(w @ w - (u @ w) ** 2 / uu, 0.0)) * (1.0 + 1e-6) if uu > 0 else 0.0
+                if uu > 0 and _exit_quad(pieces, K["box"], K["lo"], K["hi"], a0, b, K["delta"] + beta) > 0:
+                    res = 1
+            if res:
+                return res > 0, rows[:j + 1], extra[:j + 1]
+        a_in, a0, a = b_in, a, b
+    return False, rows, extra
+
+
+def _seg_dist(P, A, B):
+    """distance from each point P[i] to the polyline of segments A[k] -> B[k]"""
+    AB = B - A
+    L2 = np.maximum((AB * AB).sum(1), 1e-300)
+    t = np.clip(((P[:, None, :] - A[None]) * AB[None]).sum(2) / L2[None], 0.0, 1.0)
+    Q = A[None] + t[..., None] * AB[None]
+    return np.sqrt(((P[:, None, :] - Q) ** 2).sum(2)).min(1)
+
+
+def deviation(bh, spin, axis, o, d, coarse_extra, stretch_steps=4):
+    """Distance between the exact march's chords and the coarse march's up to the coarse march's
+    last point (by arc length): the exact points' largest distance from the coarse chords, and the
+    coarse points' from the exact chords, the larger of the two."""
+    n = len(coarse_extra)
+    rows, extra = O.kerr_chain_st(bh, spin, axis, o, d, 1.0, max_rows=int(n * stretch_steps * 1.25) + 4)
+    C = np.vstack([np.asarray(o, np.float64)[None], coarse_extra[:, 1:4]])
+    E = np.vstack([np.asarray(o, np.float64)[None], extra[:, 1:4]])
+    if len(C) < 2 or len(E) < 2:
+        return 0.0
+    lc = np.concatenate([[0.0], np.cumsum(np.linalg.norm(np.diff(C, axis=0), axis=1))])
+    le = np.concatenate([[0.0], np.cumsum(np.linalg.norm(np.diff(E, axis=0), axis=1))])
+    Ein = E[le <= lc[-1]]
+    Cin = C[:-1][lc[:-1] <= le[-1]]
+    d1 = _seg_dist(Ein, C[:-1], C[1:]).max() if len(Ein) else 0.0
+    d2 = _seg_dist(Cin, E[:-1], E[1:]).max() if len(Cin) else 0.0
+    return float(max(d1, d2))

@@ -60,6 +60,8 @@ def lib():
         L.ro_keyed_rand.argtypes = [C.c_uint64, C.c_uint32]
         L.ro_micro_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int]
         L.ro_kerr_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int, _f64p]
+        L.ro_kerr_chain_st.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int, _f64p, C.c_double, _f64p]
+        L.ro_shadow_query.argtypes = [C.c_void_p, C.POINTER(Params), _f64p, _f64p]
         L.ro_bbox_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_double, C.c_double,
                                         C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.ro_tri_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.POINTER(C.c_double), _f64p, _f64p]
@@ -148,6 +150,23 @@ def kerr_chain(bh, spin, axis, o, d, max_rows=64):
     frame = np.zeros(9, np.float64)
     n = lib().ro_kerr_chain(b, np.asarray(o, np.float64), np.asarray(d, np.float64), out, max_rows, frame)
     return out[:n], frame.reshape(3, 3)
+
+
+def kerr_chain_st(bh, spin, axis, o, d, st, max_rows=64):
+    """kerr_chain with steps st times longer (the Kerr occlusion proof's coarse march): rows as
+    kerr_chain's and extra [n, 4] = (swept polar angle after the step, segment end point)."""
+    b = np.array(list(bh) + [spin] + list(axis), np.float64)
+    out = np.zeros((max_rows, 14), np.float64)
+    extra = np.zeros((max_rows, 4), np.float64)
+    frame = np.zeros(9, np.float64)
+    n = lib().ro_kerr_chain_st(b, np.asarray(o, np.float64), np.asarray(d, np.float64), out, max_rows, frame, st,
+                               extra)
+    return out[:n], extra[:n]
+
+
+def shadow_query(scene, params, o, d):
+    """BVHAccel::intersect's boolean for the ray (o, d) under params' spacetime (restatement)."""
+    return bool(lib().ro_shadow_query(scene.h, C.byref(params), np.asarray(o, np.float64), np.asarray(d, np.float64)))
 
 
 def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):

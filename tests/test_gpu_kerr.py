@@ -29,7 +29,7 @@ KERR_CASES = [
 ]
 VARIANTS = {"default": 0, "plain": rrt.RRT_RENDER_NO_CLEAN | rrt.RRT_RENDER_NO_SKIP,
             "perpixel": rrt.RRT_RENDER_PER_PIXEL, "loop": rrt.RRT_RENDER_PIXEL_LOOP,
-            "onequeue": rrt.RRT_RENDER_ONE_QUEUE}
+            "onequeue": rrt.RRT_RENDER_ONE_QUEUE, "noproof": rrt.RRT_RENDER_NO_SHADOW_PROOF}
 _oracle_cache = {}
 
 
@@ -120,7 +120,7 @@ def cfg5_region(c, sub):
     return None if sub is None else (c.x0 + sub[0], c.y0 + sub[1], sub[2], sub[3])
 
 
-@pytest.mark.parametrize("variant", ["default", "onequeue"])
+@pytest.mark.parametrize("variant", ["default", "onequeue", "noproof"])
 @pytest.mark.parametrize("name,sub", CFG5)
 def test_kerr_cfg5_framing(gpu, name, sub, variant):
     """The benched cfg5 workload's own framing: GPU == restatement bit for bit (RGB, sample
