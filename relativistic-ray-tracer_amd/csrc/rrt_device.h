@@ -1279,7 +1279,10 @@ __device__ __forceinline__ v3 pixel_ray_dir(const KParams& kp, double sx, double
   const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
   return unit(w);
 }
-__device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px, uint32_t py) {
+// A rectangle of pixels (the strip pass, rrt_strip_proof_kernel): jitter positions [px, px + w] x
+// [py, py + h]; the same argument with the rectangle's corners and centre (the curvature term
+// uses its half-diagonal, so it holds for any small rectangle; w = h = 1 is pixel_miss_proof).
+__device__ __forceinline__ bool rect_miss_proof(const KParams& kp, double px, double py, double w, double hgt) {
 #pragma clang fp contract(fast)
   const DMissProof& mp = kp.miss;
   const DHole& h = kp.hole;
@@ -1288,7 +1291,7 @@ __device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px,
   const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
   const v3 X = vmul(x0, u0);
   // the pixel's directions: dx range, the centre's plane axis y_c and the spread of y
-  const v3 dc = pixel_ray_dir(kp, px + 0.5, py + 0.5);
+  const v3 dc = pixel_ray_dir(kp, px + 0.5 * w, py + 0.5 * hgt);
   const double dxc = dot(dc, X);
   v3 Yc = dc - smul(dxc, X);
   const double dyc = sqrt(norm2(Yc));
@@ -1297,7 +1300,7 @@ __device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px,
   double dlo = dxc, dhi = dxc, dY = 0.0, dd = 0.0;
 #pragma unroll 1
   for (int k = 0; k < 4; ++k) {
-    const v3 d = pixel_ray_dir(kp, (double)px + (k & 1), (double)py + (k >> 1));
+    const v3 d = pixel_ray_dir(kp, px + (k & 1) * w, py + (k >> 1) * hgt);
     const double dx = dot(d, X);
     dlo = fmin(dlo, dx);
     dhi = fmax(dhi, dx);
@@ -1383,6 +1386,9 @@ __device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px,
     rp = r; dpa = dpb; dvp = dv; ea = na; eb = nb;
   }
   return true;
+}
+__device__ __forceinline__ bool pixel_miss_proof(const KParams& kp, uint32_t px, uint32_t py) {
+  return rect_miss_proof(kp, (double)px, (double)py, 1.0, 1.0);
 }
 
 // Heavy pixel (slot-parallel heavy pixels): some of the pixel's rays are captured

@@ -32,7 +32,12 @@ hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, i
 hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
-hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream);
+hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, bool strips, hipStream_t stream);
+// The pixel pass's first level (rrt_sample.hip rrt_strip_proof_kernel): strips of 64 claim indices
+// proven as wholes before the per-pixel level; 0 for the per-pixel pass alone (A/B)
+#ifndef RRT_STRIP_PASS
+#define RRT_STRIP_PASS 1
+#endif
 hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_path(const KParams* d_kp, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
@@ -118,6 +123,8 @@ struct rrt_ctx {
   hipStream_t fence_stream = nullptr;
   // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
   uint32_t* d_heavy_list = nullptr;
+  uint32_t* d_strip_list = nullptr;  // the pixel pass's strips left to the per-pixel level
+  size_t strip_list_cap = 0;
   size_t heavy_list_cap = 0;
   float* d_path_stack = nullptr;  // the path pool kernel's per-level terms (rrt_path.hip)
   size_t path_stack_cap = 0;      // bytes
@@ -292,6 +299,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipFree(c->d_counter); hipFree(c->d_kp); hipFree(c->d_tiles); hipFree(c->d_order); hipFree(c->d_first); hipFree(c->d_list); hipFree(c->d_rgb); hipFree(c->d_cnt); hipFree(c->d_draws);
     hipFree(c->d_ctr);
     hipFree(c->d_heavy_list);
+    hipFree(c->d_strip_list);
     hipFree(c->d_path_stack);
     for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
       if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
@@ -1631,6 +1639,16 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       kp.claim_count = c->d_counter + RRT_QUEUE_STRIDE * RRT_MAX_QUEUES;
     }
   }
+  // the pass's strip level: tiles whose rows split into strips of 64 claim indices (ts | 64 or 64 | ts)
+  if (kp.claim_list && RRT_STRIP_PASS && (64u % ts == 0u || ts % 64u == 0u) && kp.n_pixels >= 64u) {
+    const size_t ns = kp.n_pixels / 64u;
+    if (c->strip_list_cap < ns) {
+      hipFree(c->d_strip_list); c->d_strip_list = nullptr;
+      HIPCHK(c, hipMalloc(&c->d_strip_list, sizeof(uint32_t) * ns));
+      c->strip_list_cap = ns;
+    }
+    kp.strip_list = c->d_strip_list;
+  }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (path_pool) {  // 256 paths a block, the resident blocks only (each path holds a stack slot)
@@ -1703,7 +1721,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     if (kp.first)
       HIPCHK(c, rrt_launch_first(kp, c->d_kp, lean, fw, std::min<uint32_t>((kp.n_pixels + 255) / 256, (uint32_t)c->n_cu * 8u),
                                  stream));
-    if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, kp.strip_list != nullptr, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     uint32_t bgrid = grid;
     if (kp.heavy_list) {
@@ -1741,19 +1759,19 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   } else if (path_pool) {
     std::snprintf(name, sizeof(name), "%srrt_path_kernel<%d>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   (waves >= 2 && waves <= 4) ? waves : RRT_PATH_WAVES);
-    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, kp.strip_list != nullptr, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_path(c->d_kp, waves, grid, stream));
   } else if (pixel_loop) {
     std::snprintf(name, sizeof(name), "%srrt_render_kernel<%s, %s, %d, ...>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   tf[deep || sw], tf[count], lean == 2 ? 0 : lean);
-    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, kp.strip_list != nullptr, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_render(kp, c->d_kp, deep, count, lean, waves, grid, stream));
   } else {
     std::snprintf(name, sizeof(name), "%srrt_sample_kernel<%s, %d, %d, %s>", deep_list ? "rrt_pixel_proof_kernel + " : "",
                   tf[count], lean, deep_sample ? (waves == 2 || waves == 4 ? waves : 3) : waves, tf[deep_sample]);
-    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, stream));
+    if (deep_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, kp.strip_list != nullptr, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
     HIPCHK(c, rrt_launch_sample(kp, c->d_kp, count, lean, waves, grid, stream));
   }

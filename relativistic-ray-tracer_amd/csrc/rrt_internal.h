@@ -239,6 +239,9 @@ struct KParams {
   // issue priority 2, four times as long priority 3 (rrt_sample.hip tail_prio)
   uint32_t prio_ticks, prio_pad;
   DKerrProof kproof;      // Kerr builds: the shadow rays' occlusion proof (kp.occ's face triangles)
+  // the pixel pass's first level (rrt_strip_proof_kernel): strips of 64 consecutive claim indices
+  // proven as wholes -- flag 1 per strip -- before the per-pixel level (null: per-pixel pass only)
+  uint32_t* strip_list;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

@@ -977,10 +977,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 // adaptive check (raytrace_pixel, part1_code.cpp:147-158) with count = min(ns_aa,
 // samples_per_batch) and count * draws_miss draws -- written here.  The others go to the claim
 // list, appended per wave (one atomic) so claims keep their order within each wave's run.
-__global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __restrict__ kpp) {
-  const KParams& kp = *kpp;
+// Claim index ix of the pass (a whole wave calls it together: ballots and one atomic per wave).
+__device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, uint32_t lane) {
   using namespace rrt;
-  const uint32_t ix = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   bool listed = false, heavy = false;
   if (ix < kp.n_pixels) {
@@ -1040,7 +1039,48 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
   base = __shfl(base, 0);
   if (listed) kp.claim_list[base + (uint32_t)__popcll(b & lt)] = ix | (hint << 31);
 }
-hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, hipStream_t stream) {
+// The per-pixel pass: every claim index (one lane each); behind the strip pass, the wave of a
+// proven strip (its 64 claim indices) leaves at once.  Waves run in claim-index order, so the
+// claim list keeps the batch kernel's centre-first order.
+__global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
+  const uint32_t ix = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
+  if (kp.strip_list && ix / 64u < kp.n_pixels / 64u && kp.strip_list[ix / 64u]) return;  // wave-uniform
+  pixel_pass_one(kp, ix, lane);
+}
+// First level of the pixel pass: one lane per strip of 64 consecutive claim indices
+// -- 64 / ts full rows of a tile (ts <= 64) or 64 pixels of one row (ts >= 64) -- proven as a
+// whole by rect_miss_proof; a proven strip's pixels get the pass's result for a proven pixel and
+// its flag (kp.strip_list[s] = 1) sends the per-pixel pass's wave away; the others (and strips
+// that leave the clip region) stay with the per-pixel pass.
+__global__ __launch_bounds__(256) void rrt_strip_proof_kernel(const KParams* __restrict__ kpp) {
+  const KParams& kp = *kpp;
+  using namespace rrt;
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  if (s < kp.n_pixels / 64u) {
+    const uint32_t ix0 = s * 64u, tl = kp.tile_order[ix0 / tpix], r0 = ix0 % tpix;
+    const uint32_t w = ts < 64u ? ts : 64u, hh = 64u / w;
+    const uint32_t x = kp.tiles[2 * tl] + r0 % ts, y = kp.tiles[2 * tl + 1] + r0 / ts;
+    const bool inside = x >= kp.clip_x0 && y >= kp.clip_y0 && x + w <= kp.clip_x1 && y + hh <= kp.clip_y1;
+    if (inside && rect_miss_proof(kp, (double)x, (double)y, (double)w, (double)hh)) {
+      const uint32_t n = min(kp.ns_aa, kp.samples_per_batch);
+      for (uint32_t k = 0; k < 64u; ++k) {
+        const uint32_t slot = tl * tpix + r0 + k;
+        kp.rgb[3 * slot] = 0.0f; kp.rgb[3 * slot + 1] = 0.0f; kp.rgb[3 * slot + 2] = 0.0f;
+        kp.count[slot] = (int32_t)n;
+        if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
+      }
+      kp.strip_list[s] = 1u;
+    } else {
+      kp.strip_list[s] = 0u;
+    }
+  }
+}
+// strips: the two-level pass (kp.strip_list set: the strip flags)
+hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, bool strips, hipStream_t stream) {
+  if (strips)
+    hipLaunchKernelGGL(rrt_strip_proof_kernel, dim3((n_pixels / 64u + 255) / 256), dim3(256), 0, stream, d_kp);
   hipLaunchKernelGGL(rrt_pixel_proof_kernel, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_kp);
   return hipGetLastError();
 }

@@ -78,3 +78,55 @@ def test_proven_pixels_miss(name, min_share):
             assert not _loose_root_hit(lo, hi, out[:k]).any(), (name, px, py, jx, jy)
     print(name, "proven pixels", proven / N_PIX)
     assert proven / N_PIX >= min_share
+
+
+@pytest.mark.parametrize("name,w,h,min_share", [("cfg3_bunny_1080p_s64", 32, 2, 0.1), ("cfg4_knot_4k_s256_crop", 32, 2, 0.4),
+                                                ("cfg2_spheres_1080p_s64_flat", 32, 2, 0.0), ("cfg3_bunny_1080p_s64", 8, 8, 0.3)])
+def test_proven_strips_miss(name, w, h, min_share):
+    """The pass's strip level (rrt_strip_proof_kernel: rect_miss_proof on a w x h rectangle of
+    pixels, the strips of 64 claim indices): every pixel of a proven strip -- its corners and a
+    random jitter each -- misses.  A wide strip proves less than its pixels do (its rays' v cross
+    zero at different steps), so the per-pixel level stays behind it."""
+    c = Case(name)
+    bh = np.array(c.cfg["bh"], np.float64)
+    r = rrt.Renderer(device=-1)
+    r.set_scene(rrt.SceneFile(c.scene_path))
+    boxes, _, _ = r.bvh()
+    r.close()
+    lo, hi = boxes[0][:3].copy(), boxes[0][3:].copy()
+    K = constants(bh, lo, hi)
+    cam = O.load_camera(c.camera_path)
+    cols = np.array(cam.c2w, np.float64).reshape(3, 3).T.ravel().copy()
+    pos = np.array(cam.pos, np.float64)
+    W, H = c.frame_w, c.frame_h
+    mn, mx = C.c_double(), C.c_double()
+
+    def ray(sx, sy):
+        o, d = np.zeros(3), np.zeros(3)
+        O.lib().ro_camera_ray(cam.hFov, cam.vFov, pos, cols, cam.nClip, cam.fClip, sx / W, sy / H, o, d,
+                              C.byref(mn), C.byref(mx))
+        return o, d
+
+    g = np.random.default_rng(9)
+    out = np.zeros((K["steps"] + 1, 8))
+    n_strips, proven, px_proven = 60, 0, 0
+    for _ in range(n_strips):
+        x0 = int(g.integers(0, W - w + 1)) // w * w
+        y0 = int(g.integers(0, H - h + 1)) // h * h
+        o, dc = ray(x0 + 0.5 * w, y0 + 0.5 * h)
+        corners = np.array([ray(x0 + (k & 1) * w, y0 + (k >> 1) * h)[1] for k in range(4)])
+        pix = [(x0 + i, y0 + j) for j in range(h) for i in range(w)]
+        px_ok = sum(prove(K, o, ray(px + 0.5, py + 0.5)[1],
+                          np.array([ray(px + (k & 1), py + (k >> 1))[1] for k in range(4)])) for px, py in pix[::7])
+        px_proven += px_ok
+        if not prove(K, o, dc, corners):
+            continue
+        proven += 1
+        for px, py in pix:
+            for jx, jy in [(0.0, 0.0), (1.0, 1.0), tuple(g.random(2))]:
+                o2, d2 = ray(px + jx, py + jy)
+                k = O.lib().ro_micro_chain(bh, o2, d2, out, K["steps"] + 1)
+                assert not _loose_root_hit(lo, hi, out[:k]).any(), (name, px, py, jx, jy)
+    per_px = px_proven / (n_strips * len(range(0, w * h, 7)))
+    print(name, w, h, "proven strips", proven / n_strips, "pixel level (every 7th pixel)", per_px)
+    assert proven / n_strips >= min_share
