@@ -1640,7 +1640,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
   }
   // the pass's strip level: tiles whose rows split into strips of 64 claim indices (ts | 64 or 64 | ts)
-  if (kp.claim_list && RRT_STRIP_PASS && (64u % ts == 0u || ts % 64u == 0u) && kp.n_pixels >= 64u) {
+  if (kp.claim_list && RRT_STRIP_PASS && (RRT_CLAIM_BLOCK8 || 64u % ts == 0u || ts % 64u == 0u) && kp.n_pixels >= 64u) {
     const size_t ns = kp.n_pixels / 64u;
     if (c->strip_list_cap < ns) {
       hipFree(c->d_strip_list); c->d_strip_list = nullptr;

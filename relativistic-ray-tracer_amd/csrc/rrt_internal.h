@@ -148,6 +148,24 @@ struct DKerrProof {
   uint32_t on;
 };
 
+// Claim order within a tile (every kernel that turns a claim index ix into a pixel: tile
+// tile_order[ix / ts^2], then claim_r(ix % ts^2) = the pixel's row-major index in the tile): 8x8
+// blocks in row-major order, row-major inside each (ts is a multiple of 8), so 64 consecutive
+// claims -- a wave of the pixel pass, a strip of its first level -- are a square of pixels.
+// 0: row-major claims (A/B).
+#ifndef RRT_CLAIM_BLOCK8
+#define RRT_CLAIM_BLOCK8 1
+#endif
+__host__ __device__ __forceinline__ uint32_t claim_r(uint32_t c, uint32_t ts) {
+#if RRT_CLAIM_BLOCK8
+  const uint32_t b = c >> 6, w = c & 63u, nb = ts >> 3;
+  return ((b / nb) * 8u + (w >> 3)) * ts + (b % nb) * 8u + (w & 7u);
+#else
+  (void)ts;
+  return c;
+#endif
+}
+
 #define RRT_MAX_QUEUES 8
 #define RRT_QUEUE_STRIDE 16  // counters 64 B apart
 

@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* _
       mine = e < n_list;
       const uint32_t ix = mine ? (kp.claim_list[e] & 0x7fffffffu) : 0u;
       t = kp.tile_order[ix / tpix];
-      lx = (ix % tpix) % kp.tile_size; ly = (ix % tpix) / kp.tile_size;
+      const uint32_t r = claim_r(ix % tpix, kp.tile_size);
+      lx = r % kp.tile_size; ly = r / kp.tile_size;
     } else {
       if (blk >= kp.n_blocks) break;
       t = blk / (bpt * bpt);

@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_path_kernel(const KParams* __r
         } else {
           const uint32_t ix = kp.claim_list ? (kp.claim_list[c] & 0x7fffffffu) : c;
           const uint32_t pi = ix < kp.n_pixels ? ix : 0u;
-          const uint32_t tl = kp.tile_order[pi / tpix], r = pi % tpix;
+          const uint32_t tl = kp.tile_order[pi / tpix], r = claim_r(pi % tpix, ts);
           const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
           if (ix < kp.n_pixels && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
             *rec(0) = x | (y << 16);

@@ -219,7 +219,8 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
           listed = e < *kp.claim_count;
           const uint32_t ix = listed ? (kp.claim_list[e] & 0x7fffffffu) : 0u;
           tl = kp.tile_order[ix / tpix];
-          lx = (ix % tpix) % kp.tile_size; ly = (ix % tpix) / kp.tile_size;
+          const uint32_t r = claim_r(ix % tpix, kp.tile_size);
+          lx = r % kp.tile_size; ly = r / kp.tile_size;
         } else {
           tl = pool_blk / (bpt * bpt);
           const uint32_t b = pool_blk % (bpt * bpt);
@@ -413,7 +414,7 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit, S1 = Dh / Dm;
   const DCamera& cam = kp.cam;
   const uint32_t ix = kp.heavy_list[hx];
-  const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+  const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
   const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
   const uint64_t key = rrt_pixel_key(kp.seed, x, y);
   spec ret = S(0, 0, 0);
@@ -512,7 +513,7 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
 #if RRT_PROFILE  // elapsed ticks; "rounds" 1
     if (t == 0) {
       const uint32_t ts = kp.tile_size, tpix = ts * ts;
-      const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + ix % tpix;
+      const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + claim_r(ix % tpix, ts);
       if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
     }
 #endif
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
                              : kp.n_pixels;
         const uint32_t ix = kp.claim_list ? (ent & 0x7fffffffu) : ent;
         const uint32_t pi = ix < kp.n_pixels ? ix : 0u;
-        const uint32_t tl = kp.tile_order[pi / tpix], r = pi % tpix, lx = r % ts, ly = r / ts;
+        const uint32_t tl = kp.tile_order[pi / tpix], r = claim_r(pi % tpix, ts), lx = r % ts, ly = r / ts;
         const uint32_t x = kp.tiles[2 * tl] + lx, y = kp.tiles[2 * tl + 1] + ly;
         if (ix < kp.n_pixels && x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
           if (gl == 0) {
@@ -983,7 +984,7 @@ __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, u
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   bool listed = false, heavy = false;
   if (ix < kp.n_pixels) {
-    const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+    const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
     const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
     if (x >= kp.clip_x0 && y >= kp.clip_y0 && x < kp.clip_x1 && y < kp.clip_y1) {
       if (pixel_miss_proof(kp, x, y)) {
@@ -1013,7 +1014,7 @@ __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, u
   // (the batch kernel's first hypothesis for the pixel)
   uint32_t hint = 0u;
   if (RRT_CLAIM_HYP == 2 && listed) {
-    const uint32_t tl = kp.tile_order[ix / tpix], r = ix % tpix;
+    const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
     const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
     Counters cn = {};
     hint = camera_miss_proof<false>(kp, ld3(kp.cam.pos), pixel_ray_dir(kp, x + 0.5, y + 0.5), cn) ? 0u : 1u;
@@ -1059,14 +1060,14 @@ __global__ __launch_bounds__(256) void rrt_strip_proof_kernel(const KParams* __r
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   if (s < kp.n_pixels / 64u) {
-    const uint32_t ix0 = s * 64u, tl = kp.tile_order[ix0 / tpix], r0 = ix0 % tpix;
-    const uint32_t w = ts < 64u ? ts : 64u, hh = 64u / w;
+    const uint32_t ix0 = s * 64u, tl = kp.tile_order[ix0 / tpix], r0 = claim_r(ix0 % tpix, ts);
+    const uint32_t w = RRT_CLAIM_BLOCK8 ? 8u : ts < 64u ? ts : 64u, hh = 64u / w;
     const uint32_t x = kp.tiles[2 * tl] + r0 % ts, y = kp.tiles[2 * tl + 1] + r0 / ts;
     const bool inside = x >= kp.clip_x0 && y >= kp.clip_y0 && x + w <= kp.clip_x1 && y + hh <= kp.clip_y1;
     if (inside && rect_miss_proof(kp, (double)x, (double)y, (double)w, (double)hh)) {
       const uint32_t n = min(kp.ns_aa, kp.samples_per_batch);
       for (uint32_t k = 0; k < 64u; ++k) {
-        const uint32_t slot = tl * tpix + r0 + k;
+        const uint32_t slot = tl * tpix + claim_r(ix0 % tpix + k, ts);
         kp.rgb[3 * slot] = 0.0f; kp.rgb[3 * slot + 1] = 0.0f; kp.rgb[3 * slot + 2] = 0.0f;
         kp.count[slot] = (int32_t)n;
         if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
