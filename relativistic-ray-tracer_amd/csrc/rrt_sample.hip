@@ -1050,7 +1050,8 @@ __global__ __launch_bounds__(256) void rrt_pixel_proof_kernel(const KParams* __r
   pixel_pass_one(kp, ix, lane);
 }
 // First level of the pixel pass: one lane per strip of 64 consecutive claim indices
-// -- 64 / ts full rows of a tile (ts <= 64) or 64 pixels of one row (ts >= 64) -- proven as a
+// -- an 8x8 block (claim_r; with row-major claims, 64 / ts full rows of a tile for ts <= 64 or 64
+// pixels of one row for ts >= 64) -- proven as a
 // whole by rect_miss_proof; a proven strip's pixels get the pass's result for a proven pixel and
 // its flag (kp.strip_list[s] = 1) sends the per-pixel pass's wave away; the others (and strips
 // that leave the clip region) stay with the per-pixel pass.
