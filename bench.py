@@ -63,7 +63,8 @@ WORKLOADS = {
 # that cover each workload's frame: bench.py checks the frame it timed against them bit for bit
 VERIFY = {"cfg1": ["cfg1_spheres_480x360_s8"], "cfg2": ["cfg2_spheres_1080p_s64_flat"],
           "cfg3": ["cfg3_bunny_1080p_s64"],
-          "cfg4": ["cfg4_knot_4k_s256_crop", "cfg4_knot_4k_s256_crop2", "cfg4_knot_4k_s256_crop3"]}
+          "cfg4": ["cfg4_knot_4k_s256_crop", "cfg4_knot_4k_s256_crop2", "cfg4_knot_4k_s256_crop3"],
+          "m3": ["m3_spheres_1080p_s64_crop", "m3_spheres_1080p_s64_crop2"]}
 
 
 def verify_frame(workload, rgb, cnt):
@@ -73,7 +74,7 @@ def verify_frame(workload, rgb, cnt):
     if not names:
         why = {"cfg5": "Kerr has no reference (parity unpinned); tests/test_gpu_kerr.py pins crops of this "
                        "framing against the restatement",
-               "m3": "no reference golden at this framing; tests/test_gpu_parity.py pins depth 3 at 96x72"}
+               }
         return None, why.get(workload, "no reference golden for this workload")
     notes = []
     for n in names:
@@ -116,6 +117,7 @@ def load_workload_scene(wl, workdir):
     assert rc == 0
     return scene, cam, spath, cpath
 TILE = 32
+AUDIT_EVERY_LOG2 = 10  # proof audit: every 1024th proven ray / pixel of the executed-work pass
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic bytes
 BYTES_PLANE = 32  # plane-cull record (DPlane) read per plane test
@@ -365,6 +367,12 @@ def main():
     kern_ms = []
 
     def step(timed):
+        # poison every output buffer in-stream first (NaN radiance, count -1): the frame verified
+        # after the timed steps can only come from the last of them (~33 MB per 1080p frame, ~10 us)
+        packed.fill_(-1)
+        if rank == 0:
+            frame_rgb.view(torch.int32).fill_(-1)
+            frame_cnt.fill_(-1)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -424,7 +432,16 @@ def main():
         return [float(v) for v in t.cpu().numpy()], c4
 
     (samples, bbox, micro, prim, queries, pixels), _ = count_pass(0)
+    # the executed-work pass runs the proofs: audit every 1024th proven ray (and pixel) exactly
+    r.set_proof_audit(AUDIT_EVERY_LOG2)
     (_, x_bbox, x_micro, x_prim, x_plane, _), xc4 = count_pass(rrt.RRT_RENDER_COUNT_EXECUTED)
+    r.set_proof_audit(-1)
+    audit = r.proof_audit()
+    if world > 1:
+        at = torch.tensor([[v["checked"], v["violations"]] for v in audit.values()], dtype=torch.float64, device=dev)
+        dist.all_reduce(at)
+        audit = {k: {"checked": int(at[i, 0]), "violations": int(at[i, 1])} for i, k in enumerate(audit)}
+    audit_violations = sum(v["violations"] for v in audit.values())
     loc_bytes = BYTES_AABB * xc4[0] + BYTES_PRIM * xc4[2] + BYTES_PLANE * xc4[3] + BYTES_PIXEL * pix_local
     ref_bytes = BYTES_AABB * bbox + BYTES_PRIM * prim + BYTES_PIXEL * pixels
     main_kernel = kernel_name.split(" + ")[-1]
@@ -471,6 +488,10 @@ def main():
             "main_kernel_ms_rank0": main_ms,
             "work_per_sample_reference": work,
             "work_per_sample_executed": xwork,
+            # run-time audit of the proofs (skipped marches): every 2^AUDIT_EVERY_LOG2-th proven ray
+            # of the untimed executed-work pass re-marched exactly (rrt_set_proof_audit)
+            "proof_violations": audit_violations,
+            "proof_audit": dict(audit, every=1 << AUDIT_EVERY_LOG2),
         }
         out.update(rooflines(loc_bytes, ref_bytes, main_ms, kernel_name, main_kernel, traffic, pmc,
                              out_bytes=float(BYTES_PIXEL * pix_local)))
@@ -483,6 +504,8 @@ def main():
         dist.destroy_process_group()
     if rank == 0 and verified is False:
         sys.exit("bench.py: the timed frame differs from the reference: " + verify_note)
+    if rank == 0 and audit_violations:
+        sys.exit(f"bench.py: the proof audit found {audit_violations} proven rays the exact march contradicts")
 
 
 if __name__ == "__main__":

@@ -26,12 +26,13 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 3  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
+#define RRT_ABI_VERSION 4  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
                               3: rrt_stats gained last_main_kernel_ms / last_heavy_pixels (callers
                                  built against 2 pass a smaller struct: rebuild), the
                                  RRT_RENDER_WAVEFRONT selects the path pool kernel (depth >= 2;
                                  RRT_E_INVALID elsewhere),
-                                 rrt_libm_eval added */
+                                 rrt_libm_eval added
+                              4: rrt_set_proof_audit / rrt_get_proof_audit added */
 
 enum {
   RRT_OK = 0,
@@ -328,6 +329,17 @@ int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
  * sinf/cosf (sampler.cpp:23-25)) on n host arguments: fn 0 sin(a), 1 cos(a), 2 acos(a),
  * 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a) (float results widened to double). */
 int rrt_libm_eval(rrt_ctx* ctx, int fn, const double* a, const double* b, double* out, uint64_t n);
+/* Run-time proof audit.  The renderer skips marches whose results its proofs
+ * determine (camera-ray miss, shadow-ray occlusion, pixel and strip miss, Kerr occlusion); their
+ * margins are validated by sweeps.  With the audit set, every counting launch that runs the proofs
+ * (RRT_RENDER_COUNTERS | RRT_RENDER_COUNT_EXECUTED) also marches every 2^every_log2-th proven ray
+ * (every 2^every_log2-th pixel for the pixel pass) exactly and tallies disagreements.  Render
+ * outputs are unchanged.  rrt_get_proof_audit (synchronises the device) returns and resets the
+ * tallies: out[2 k] rays checked, out[2 k + 1] violations, k = RRT_AUDIT_CAMERA .. RRT_AUDIT_KERR. */
+enum { RRT_AUDIT_CAMERA = 0, RRT_AUDIT_SHADOW = 1, RRT_AUDIT_PIXEL = 2, RRT_AUDIT_STRIP = 3, RRT_AUDIT_KERR = 4,
+       RRT_AUDIT_KINDS = 5 };
+int rrt_set_proof_audit(rrt_ctx* ctx, int every_log2 /* < 0: off (the default) */);
+int rrt_get_proof_audit(rrt_ctx* ctx, uint64_t* out /* [2 * RRT_AUDIT_KINDS] */);
 /* HIP-event times of the last n (<= 32) render launches, oldest first: the whole launch and its
  * main kernel alone (bench.py's roofline divides by the latter).  Returns the count filled. */
 int rrt_get_launch_times(const rrt_ctx* ctx, uint32_t n, float* total_ms, float* main_ms);

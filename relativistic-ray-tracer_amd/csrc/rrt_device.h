@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "rrt_internal.h"
+#include "../../include/rrt.h"  // RRT_AUDIT_* proof kinds
 #include "rrt_rng.h"
 #include "rrt_glibm.h"
 
@@ -812,11 +813,40 @@ __device__ __forceinline__ bool kerr_advance(const DHole& h, v3& q, v3& p, doubl
 // outer horizon.  Steps are sized by distance (accurate for radial motion too), so the sweep is
 // budgeted by angle, not by count (at most kerr_max_steps), and a photon moving outward beyond
 // every primitive (|q|^2 > r_esc2 >= (4M)^2, outside all photon orbits) has escaped: no hit.
+// ------------------------------------------------------------------ run-time proof audit
+// The proofs (camera miss, shadow occlusion, pixel and strip miss, Kerr occlusion) write a result
+// without marching; their margins were validated by sweeps.  A counting launch with kp.audit set
+// (rrt_set_proof_audit; bench.py's executed-work pass) re-marches every 2^audit_shift-th proven ray
+// exactly and tallies disagreements: kp.audit[2 k] rays checked, [2 k + 1] violations.
+// (proof kinds k: include/rrt.h RRT_AUDIT_*)
+__device__ __forceinline__ bool audit_pick(const KParams& kp, v3 o, v3 d) {
+  const uint64_t h = rrt_mix64((uint64_t)__double_as_longlong(d.x) ^
+                               rrt_mix64((uint64_t)__double_as_longlong(d.y) ^ ((uint64_t)__double_as_longlong(d.z) << 1)) ^
+                               ((uint64_t)__double_as_longlong(o.x) >> 2));
+  return (h & ((1ull << kp.audit_shift) - 1ull)) == 0ull;
+}
+__device__ __forceinline__ void audit_note(const KParams& kp, int k, bool violated) {
+  atomicAdd(kp.audit + 2 * k, 1u);
+  if (violated) atomicAdd(kp.audit + 2 * k + 1, 1u);
+}
 __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d);
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn);
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   // shadow rays: the occlusion proof first (never in the reference-work counts)
-  if (ANY && kp.kproof.on && !(COUNT && !kp.count_exec) && kerr_occluded_proof(kp, o, d)) return true;
+  if (ANY && kp.kproof.on && !(COUNT && !kp.count_exec) && kerr_occluded_proof(kp, o, d)) {
+    if (COUNT && kp.audit && audit_pick(kp, o, d)) {
+      Counters c2 = {};
+      audit_note(kp, RRT_AUDIT_KERR, !kerr_march<true, false>(kp, o, d, nullptr, c2));
+    }
+    return true;
+  }
+  return kerr_march<ANY, COUNT>(kp, o, d, is, cn);
+}
+// the march of query_kerr (no proof)
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   const DHole& h = kp.hole;
   v3 q, p;
   kerr_init(h, o, d, q, p);
@@ -1258,6 +1288,11 @@ __device__ __forceinline__ bool camera_proven_miss(const KParams& kp, v3 o, v3 d
   RRT_T0(tp0);
   const bool r = NI ? camera_miss_proof_call<COUNT, W>(kp, o, d, cn) : camera_miss_proof<COUNT>(kp, o, d, cn);
   RRT_ACC(t_proof, tp0);
+  if (COUNT && r && kp.audit && audit_pick(kp, o, d)) {
+    Counters c2 = {};
+    Isect i2;
+    audit_note(kp, RRT_AUDIT_CAMERA, query<false, false, false>(kp, o, d, &i2, c2));
+  }
   return r;
 }
 
@@ -1297,7 +1332,7 @@ __device__ __forceinline__ bool rect_miss_proof(const KParams& kp, double px, do
   const double dyc = sqrt(norm2(Yc));
   if (!(dyc > 1e-3)) return false;  // towards the hole: no stable plane
   Yc = vmul(Yc, 1.0 / dyc);
-  double dlo = dxc, dhi = dxc, dY = 0.0, dd = 0.0;
+  double dlo = dxc, dhi = dxc, dY = 0.0, dd = 0.0, dymin = dyc;
 #pragma unroll 1
   for (int k = 0; k < 4; ++k) {
     const v3 d = pixel_ray_dir(kp, px + (k & 1) * w, py + (k >> 1) * hgt);
@@ -1307,9 +1342,16 @@ __device__ __forceinline__ bool rect_miss_proof(const KParams& kp, double px, do
     const v3 yv = d - smul(dx, X);
     const double dy = sqrt(norm2(yv));
     if (!(dy > 1e-3)) return false;
+    dymin = fmin(dymin, dy);
     dY = fmax(dY, sqrt(norm2(vmul(yv, 1.0 / dy) - Yc)));
     dd = fmax(dd, sqrt(norm2(d - dc)));
   }
+  // Every direction of the rectangle lies within dd of dc (the farthest point of a convex spherical
+  // polygon from an inner point is a vertex), so the directions +-X -- where the plane axis y turns
+  // round -- stay outside it when dd is well below the sine of dc's angle from them, and y then
+  // varies smoothly over the rectangle, its spread set by the corners.  A rectangle subtending a
+  // large angle near +-X (small frames, wide fields of view) is left to the pixel level.
+  if (!(dd <= 0.25 * dymin)) return false;
   // a smooth function over the small square: extremes within the corners' values plus a
   // curvature term of the square's angular radius squared
   const double slack = 2.0 * dd * dd + 1e-12, wdx = dhi - dlo;
@@ -1474,7 +1516,13 @@ __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* i
     const bool occluded = RRT_SHADOW_MODE == 1 ? shadow_proof_call<W>(kp, o, d)
                                                : shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
     RRT_ACC(t_squery, tp0);
-    if (occluded) return true;
+    if (occluded) {
+      if (COUNT && kp.audit && audit_pick(kp, o, d)) {
+        Counters c2 = {};
+        audit_note(kp, RRT_AUDIT_SHADOW, !query<true, false, false>(kp, o, d, nullptr, c2));
+      }
+      return true;
+    }
   }
   if (NI && !COUNT) return query_call<ANY, KERR>(kp, o, d, is);
   return query<ANY, COUNT, KERR>(kp, o, d, is, cn);

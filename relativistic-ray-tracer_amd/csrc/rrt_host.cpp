@@ -64,6 +64,10 @@ constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_
 #define RRT_KPROOF_DT_MAX 0.1
 #define RRT_KPROOF_SPIN_MAX 0.99
 #define RRT_KPROOF_REACH_M 40.0
+#define RRT_KPROOF_CENTRE_LO 0.2
+#define RRT_KPROOF_CENTRE_HI 0.8
+#define RRT_KPROOF_RS_LO 0.04
+#define RRT_KPROOF_RS_HI 0.15
 
 struct V3 { double x, y, z; };
 inline V3 mk(double x, double y, double z) { return V3{x, y, z}; }
@@ -124,6 +128,8 @@ struct rrt_ctx {
   // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
   uint32_t* d_heavy_list = nullptr;
   uint32_t* d_strip_list = nullptr;  // the pixel pass's strips left to the per-pixel level
+  uint32_t* d_audit = nullptr;       // proof-audit tallies (rrt_set_proof_audit), 16 words
+  uint32_t audit_shift = 0;          // 0: no audit; else re-check every 2^(audit_shift - 1)-th proven ray
   size_t strip_list_cap = 0;
   size_t heavy_list_cap = 0;
   float* d_path_stack = nullptr;  // the path pool kernel's per-level terms (rrt_path.hip)
@@ -300,6 +306,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_heavy_list);
     hipFree(c->d_strip_list);
+    hipFree(c->d_audit);
     hipFree(c->d_path_stack);
     for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
       if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
@@ -1378,7 +1385,18 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     DKerrProof& kq = kp.kproof;
     kq = DKerrProof{};
     const DHole& h = kp.hole;
-    const bool kenv = h.kind == RRT_METRIC_KERR && any && fin && h.m > 0.0 && h.dt >= RRT_KPROOF_DT_MIN &&
+    // the swept region only: the hole's centre within the middle 60% of the root box on every axis
+    // and r_s within [0.04, 0.15] of its largest extent (the sweep's holes: 0.2 .. 0.8 of each axis,
+    // r_s 0.08 .. 0.3 in rooms 2 units across)
+    bool kin = true;
+    double kext = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double e = kp.miss.hi[k] - kp.miss.lo[k];
+      kext = std::max(kext, e);
+      kin = kin && h.c[k] >= kp.miss.lo[k] + RRT_KPROOF_CENTRE_LO * e && h.c[k] <= kp.miss.lo[k] + RRT_KPROOF_CENTRE_HI * e;
+    }
+    kin = kin && h.r >= RRT_KPROOF_RS_LO * kext && h.r <= RRT_KPROOF_RS_HI * kext;
+    const bool kenv = h.kind == RRT_METRIC_KERR && any && fin && kin && h.m > 0.0 && h.dt >= RRT_KPROOF_DT_MIN &&
                       h.dt <= RRT_KPROOF_DT_MAX && h.a <= RRT_KPROOF_SPIN_MAX * h.m &&
                       h.r_esc2 <= (RRT_KPROOF_REACH_M * h.m) * (RRT_KPROOF_REACH_M * h.m);
     if (kenv && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) {
@@ -1427,7 +1445,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   if (sw && kerr) return fail(c, RRT_E_INVALID, "the reference's switches (THIN_LENS, ADAPTIVE, ILLUM, ENV_HEMI, "
                                                 "MICROFACET_HEMI) are built for the Schwarzschild stepper only");
   if (sw && ((kp.sw >> 4) ^ 2u) == 3u && p->max_ray_depth == 0)
-    return fail(c, RRT_E_INVALID, "ILLUM 3 with max_ray_depth 0 recurses without end in the reference");
+    return fail(c, RRT_E_INVALID, "ILLUM 3 with max_ray_depth 0: the reference's recursion depth is unbounded there "
+                                  "(Ray::depth is size_t and wraps below 0; only Russian roulette ends it), beyond "
+                                  "RRT_MAX_DEPTH");
   if (sw) { kp.miss.on = 0u; kp.occ.on = 0u; }
   // bounce paths (depth >= 2): the per-pixel-loop kernel by default; RRT_RENDER_DEEP_SAMPLE selects
   // the per-sample refill kernel (rrt_sample.hip, one lane per pixel, a lane whose pixel is done
@@ -1440,6 +1460,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // an A/B variant: m3 269 ms at 3 waves/SIMD vs 172 ms for the per-pixel loop.
   // Its light-sample cursor holds 11 bits: n_lights x ns_area_light < 2048.
   const bool path_pool = (p->flags & RRT_RENDER_WAVEFRONT) != 0;
+  // its path records pack the pixel as x | y << 16
+  if (path_pool && (p->frame_w > 65535u || p->frame_h > 65535u))
+    return fail(c, RRT_E_INVALID, "RRT_RENDER_WAVEFRONT (the path pool kernel) renders frames of at most 65535 pixels a side");
   if (path_pool && !(deep && !count && !kerr && !sw && p->ns_aa >= 1 &&
                      (uint64_t)all_lights(c).size() * std::max<uint32_t>(1u, p->ns_area_light) < 2048u))
     return fail(c, RRT_E_INVALID, "RRT_RENDER_WAVEFRONT (the path pool kernel) renders max_ray_depth >= 2 "
@@ -1649,6 +1672,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
     kp.strip_list = c->d_strip_list;
   }
+  // run-time proof audit: counting launches that run the proofs (executed-work counts)
+  if (count && kp.count_exec && c->audit_shift && c->d_audit) {
+    kp.audit = c->d_audit;
+    kp.audit_shift = c->audit_shift - 1u;
+  }
   uint32_t want = batch ? (uint32_t)(((uint64_t)kp.n_pixels * kp.group + 255) / 256) : (kp.n_blocks + 3) / 4;
   uint32_t grid = std::min<uint32_t>(want, (uint32_t)c->n_cu * 8u);
   if (path_pool) {  // 256 paths a block, the resident blocks only (each path holds a stack slot)
@@ -1699,6 +1727,11 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // tail priority threshold (A/B: RRT_AB_PRIO_TICKS in the environment)
   kp.prio_ticks = 50000u;
   if (const char* pt = std::getenv("RRT_AB_PRIO_TICKS")) kp.prio_ticks = (uint32_t)std::strtoul(pt, nullptr, 10);
+  // dealt shadow walks in the batch kernel's LEAN builds (A/B and parity: RRT_AB_NO_DEAL=1 in the environment)
+  {
+    const char* nd = std::getenv("RRT_AB_NO_DEAL");
+    kp.deal = (nd && nd[0] == '1') ? 0u : 1u;
+  }
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
   HIPCHK(c, hipEventRecord(c->ev0[ring], stream));
@@ -1966,6 +1999,34 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
 
 // Per-launch HIP-event times of the context's last n launches (n <= 32), oldest first: the whole
 // launch and its main kernel alone.  Synchronises on the last of them.  Returns the count filled.
+extern "C" int rrt_set_proof_audit(rrt_ctx* c, int every_log2) {
+  if (!c || every_log2 > 30) return c ? fail(c, RRT_E_INVALID, "every_log2 > 30") : RRT_E_INVALID;
+  if (every_log2 < 0) {  // off
+    c->audit_shift = 0;
+    return RRT_OK;
+  }
+  if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "host-only context cannot render");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->d_audit) {
+    HIPCHK(c, hipMalloc(&c->d_audit, sizeof(uint32_t) * 16));
+    HIPCHK(c, hipMemset(c->d_audit, 0, sizeof(uint32_t) * 16));
+  }
+  c->audit_shift = (uint32_t)every_log2 + 1u;
+  return RRT_OK;
+}
+extern "C" int rrt_get_proof_audit(rrt_ctx* c, uint64_t* out) {
+  if (!c || !out) return RRT_E_INVALID;
+  for (int k = 0; k < 2 * RRT_AUDIT_KINDS; ++k) out[k] = 0;
+  if (!c->d_audit) return RRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t h[16];
+  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, hipMemcpy(h, c->d_audit, sizeof(h), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemset(c->d_audit, 0, sizeof(h)));
+  for (int k = 0; k < 2 * RRT_AUDIT_KINDS; ++k) out[k] = h[k];
+  return RRT_OK;
+}
+
 extern "C" int rrt_get_launch_times(const rrt_ctx* cc, uint32_t n, float* total_ms, float* main_ms) {
   rrt_ctx* c = const_cast<rrt_ctx*>(cc);
   if (!c || (n && (!total_ms || !main_ms))) return RRT_E_INVALID;

@@ -255,11 +255,17 @@ struct KParams {
   float* path_stack;
   // batch kernel: a wave whose oldest pixel has run this long (wall-clock ticks, 100 MHz) takes
   // issue priority 2, four times as long priority 3 (rrt_sample.hip tail_prio)
-  uint32_t prio_ticks, prio_pad;
+  uint32_t prio_ticks;
+  uint32_t deal;  // batch kernel: dealt shadow walks (rrt_sample.hip shadow_dealt); RRT_AB_NO_DEAL=1 turns them off
   DKerrProof kproof;      // Kerr builds: the shadow rays' occlusion proof (kp.occ's face triangles)
   // the pixel pass's first level (rrt_strip_proof_kernel): strips of 64 consecutive claim indices
   // proven as wholes -- flag 1 per strip -- before the per-pixel level (null: per-pixel pass only)
   uint32_t* strip_list;
+  // run-time proof audit (rrt_device.h audit_pick): counting launches re-check every
+  // 2^audit_shift-th proven ray (and pixel) against the exact march; tallies [2 k] checked,
+  // [2 k + 1] violations per proof k (RRT_AUDIT_*); null: no audit
+  uint32_t* audit;
+  uint32_t audit_shift, audit_pad;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

@@ -110,6 +110,148 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
   return direct_hemisphere_parked<COUNT, LEAN>(kp, g, cl, t, cn);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Segment-parallel shadow queries ("dealt walks").  BVHAccel::intersect
+// (bvh.cpp:103-113) marches a chain of micro segments; each segment depends only on the one before
+// (BlackHole::next_micro_ray, blackhole.cpp:17-40), never on a walk's result, and a shadow query is
+// true iff some segment before the capture hits a primitive.  So the chain can be generated first
+// and its walks run in any order, by any lanes.  In the batch kernel a wave's unproven shadow rays
+// are few (the occlusion proof takes most), and marched lane by lane their walks run one micro step
+// at a time while the wave's other lanes idle.  Here the wave's rays generate their chains in
+// lock-step, the segments that need a walk (not captured before, not skipped: outside the root box
+// or in clear grid cells) go to a per-wave LDS list, and when the list is full (or every chain has
+// ended) each lane of the wave walks one listed segment; a ray stops generating once one of its
+// walks has hit.  The answer is the reference's: hit <=> some uncaptured segment's walk hits.
+#ifndef RRT_DEAL
+#define RRT_DEAL 1  // 0: build without the dealt shadow walks (A/B)
+#endif
+#ifndef RRT_DEAL_CAP
+#define RRT_DEAL_CAP 32  // listed segments per wave (LDS: 60 B each)
+#endif
+template <uint32_t CAP>
+struct DealLds {  // per wave: micro segments waiting for a walk (structure of arrays)
+  double o[3][CAP], d[3][CAP], mt[CAP];
+  uint32_t ray[CAP];
+  unsigned long long occ;  // lanes whose query found a hit
+};
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// The shadow query (BVHAccel::intersect without an Intersection) of every lane with need set;
+// all 64 lanes of the wave call it together.  Returns the query's result for those lanes.
+#ifndef RRT_DEAL_INLINE
+#define RRT_DEAL_INLINE 0  // 1: shadow_dealt inlined into the batch kernel (A/B)
+#endif
+#if RRT_DEAL_INLINE
+#define RRT_DEAL_ATTR __forceinline__
+#else
+#define RRT_DEAL_ATTR __noinline__
+#endif
+template <uint32_t CAP>
+__device__ RRT_DEAL_ATTR bool shadow_dealt(const KParams& kp, v3 o, v3 d, bool need, DealLds<CAP>& dl, uint32_t lane) {
+  static_assert(CAP <= 64, "one listed segment per lane and drain");
+  if (__ballot(need) == 0) return false;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (lane == 0) lput(&dl.occ, 0u, 0ull);
+  wave_sync_lds();
+  v3 e = o;
+  double max_t = 0.0;
+  int j = 0;
+  bool gen = need;
+#pragma unroll 1
+  for (;;) {
+    uint32_t n = 0;  // listed segments (wave-uniform)
+    // generate: every chain one micro step per pass, while the list has room for a segment of each
+#pragma unroll 1
+    for (;;) {
+      const uint64_t gm = __ballot(gen);
+      if (gm == 0 || n + (uint32_t)__popcll(gm) > CAP) break;
+      bool want = false;
+      if (gen) {
+        v3 rel;
+        double rel2;
+        next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
+        ++j;
+        if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) {  // captured: the query ends without a hit
+          gen = false;
+        } else {
+          e = o + vmul(d, max_t);
+          want = !segment_outside_root(kp, o, e) && !cell_clear(kp.grid, grid_cell(kp.grid, o), max_t);
+          if (j >= kp.hole.steps) gen = false;
+        }
+      }
+      const uint64_t wm = __ballot(want);
+      if (want) {
+        const uint32_t k = n + (uint32_t)__popcll(wm & lt);
+        lput(dl.o[0], k, o.x); lput(dl.o[1], k, o.y); lput(dl.o[2], k, o.z);
+        lput(dl.d[0], k, d.x); lput(dl.d[1], k, d.y); lput(dl.d[2], k, d.z);
+        lput(dl.mt, k, max_t); lput(dl.ray, k, lane);
+      }
+      n += (uint32_t)__popcll(wm);
+    }
+    if (n == 0) break;  // every chain has ended and nothing is listed
+    wave_sync_lds();
+    // drain: lane k walks listed segment k (a ray already known to hit is skipped)
+    if (lane < n) {
+      const uint32_t r = lget(dl.ray, lane);
+      if (!((lget(&dl.occ, 0u) >> r) & 1ull)) {
+        const v3 so = V(lget(dl.o[0], lane), lget(dl.o[1], lane), lget(dl.o[2], lane));
+        const v3 sd = V(lget(dl.d[0], lane), lget(dl.d[1], lane), lget(dl.d[2], lane));
+        const double smt = lget(dl.mt, lane);
+        Counters cn = {};
+        if (segment_walk<true, false>(kp, so, sd, smt, so + vmul(sd, smt), grid_cell(kp.grid, so), nullptr, cn))
+          atomicOr(&dl.occ, 1ull << r);
+      }
+    }
+    wave_sync_lds();
+    if ((lget(&dl.occ, 0u) >> lane) & 1ull) gen = false;  // a hit: the query is true
+    if (__ballot(gen) == 0) break;
+  }
+  return need && ((lget(&dl.occ, 0u) >> lane) & 1ull);
+}
+
+// estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS, with every
+// lane of the wave taking part (act: this lane shades a hit): the occlusion proof per lane, then the
+// unproven shadow rays through shadow_dealt.  Same draws, same sums as direct_importance_parked.
+template <int LEAN, int W, uint32_t CAP, class SL>
+__device__ spec direct_importance_wave(const KParams& kp, Rng& g, SL& cl, uint32_t t, bool act, DealLds<CAP>& dl) {
+  const uint32_t lane = t & 63u;
+  spec L = S(0, 0, 0);
+  int total = 0;
+  for (uint32_t li = 0; li < kp.n_lights; ++li) {
+    const uint32_t is_delta_l = kp.lights[li].is_delta;
+    const int num = is_delta_l ? 1 : (int)kp.ns_area_light;
+    total += num;
+    for (int i = 0; i < num; ++i) {
+      bool need = false;
+      v3 so = V(0.0, 0.0, 0.0), sd = V(0.0, 0.0, 1.0);
+      if (act) {
+        const uint32_t bsdf = lget(cl.bsdf, t);
+        const v3 hp = V(lget(cl.hp[0], t), lget(cl.hp[1], t), lget(cl.hp[2], t));
+        const v3 nn = V(lget(cl.nn[0], t), lget(cl.nn[1], t), lget(cl.nn[2], t));
+        const v3 wo = V(lget(cl.wo[0], t), lget(cl.wo[1], t), lget(cl.wo[2], t));
+        v3 wi_world; float dist, pdf;
+        const spec sample = light_sample_L<LEAN>(kp.env, kp.lights[li], g, hp, wi_world, dist, pdf);
+        const Frame f = coord_space(nn);
+        const v3 w_in = to_local(f, wi_world);
+        if (!(w_in.z < 0)) {
+          const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
+          lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
+          so = hp + smul(EPS_D, wi_world);
+          sd = wi_world;
+          // the occlusion proof first (rrt_device.h query_nx): a proven ray is occluded
+          need = !(RRT_SHADOW_PROOF && W && kp.occ.on && shadow_occluded_proof<W>(kp, so, sd, kp.hole.steps));
+        }
+      }
+      const bool occluded = shadow_dealt<CAP>(kp, so, sd, need, dl, lane);
+      if (need && !occluded) L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
+    }
+  }
+  return L / (float)total;
+}
+
 }  // namespace rrt
 
 // The shadow-ray occlusion proof's build tag (rrt_device.h query_nx): the area-light and the
@@ -177,6 +319,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
   bool pool_empty = false;
   bool have = false;                      // lane holds a pixel
   uint32_t px = 0, py = 0, slot = 0;
+  uint32_t aud = 0;  // proof audit (COUNT): bit 0 the pixel's miss proof holds, bit 1 its strip's
   int i = 0;                              // samples done for the lane's pixel
   Rng g; g.key = 0; g.ctr = 0;
   Counters cn = {};
@@ -236,6 +379,18 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
           lput(cl.s1, t, 0.0); lput(cl.s2, t, 0.0);
           lput(cl.rr, t, 0.0f); lput(cl.rg, t, 0.0f); lput(cl.rb, t, 0.0f);
           have = true;
+          aud = 0;
+          // audit of the pixel pass (rrt_pixel_proof_kernel / rrt_strip_proof_kernel, whose proven
+          // pixels the batch kernel never marches): on every 2^audit_shift-th pixel, whether its
+          // proofs hold; every camera ray of such a pixel is then marched exactly below
+          if (COUNT && kp.audit && kp.miss.on &&
+              (rrt_mix64(g.key) & ((1ull << kp.audit_shift) - 1ull)) == 0ull) {
+            if (pixel_miss_proof(kp, x, y)) aud |= 1u;
+            const uint32_t sx = kp.tiles[2 * tl] + (lx & ~7u), sy = kp.tiles[2 * tl + 1] + (ly & ~7u);
+            if (RRT_CLAIM_BLOCK8 && sx >= kp.clip_x0 && sy >= kp.clip_y0 && sx + 8u <= kp.clip_x1 && sy + 8u <= kp.clip_y1 &&
+                rect_miss_proof(kp, (double)sx, (double)sy, 8.0, 8.0))
+              aud |= 2u;
+          }
           if (kp.ns_aa == 0) {  // the reference's loop does not run: ret / 0, count 0
             const float r = 0.0f / (float)0;
             kp.rgb[3 * slot] = r; kp.rgb[3 * slot + 1] = r; kp.rgb[3 * slot + 2] = r;
@@ -272,6 +427,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         else s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
       } else if (!is_lean(LEAN) && kp.env.w) {
         s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
+      }
+      if (COUNT && aud) {  // the pixel pass's proofs say this camera ray misses
+        Counters c2 = {};
+        Isect i2;
+        const bool ex = query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &i2, c2);
+        if (aud & 1u) audit_note(kp, RRT_AUDIT_PIXEL, ex);
+        if (aud & 2u) audit_note(kp, RRT_AUDIT_STRIP, ex);
       }
     }
     const spec ret = S(lget(cl.rr, t), lget(cl.rg, t), lget(cl.rb, t)) + s;
@@ -551,6 +713,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   // the claim space (a multiple of 64 pixels: tiles of 8k x 8k) must hold whole stripes
   static_assert(STRIPE > 0 && 64u % STRIPE == 0, "RRT_STRIPE must divide 64");
   __shared__ GroupLds<RRT_SLOTS> gs;
+  // the area-light build at <= 4 waves/SIMD (LDS: 4 blocks of 28.5 + 7.7 KB a CU); not the point-light
+  // build (no occlusion proof, few shadow rays: cfg4's frame is its camera rays)
+  constexpr bool DEAL = RRT_DEAL && LEAN == 1 && WAVES <= 4;
+  constexpr uint32_t DCAP = DEAL ? (uint32_t)RRT_DEAL_CAP : 1u;
+  __shared__ DealLds<DCAP> dl[4];  // one per wave (shadow_dealt)
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
   float* const fg = cl.cg;
   float* const fb = cl.cb;
@@ -871,7 +1038,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
       s = env_dir(kp.env, unit(w));
     }
-    if (act && hit) {
+    if (DEAL && kp.deal && kp.max_ray_depth != 0) {
+      // every lane takes part: the unproven shadow rays' walks are dealt over the wave (shadow_dealt)
+      const bool shade = act && hit;
+      Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
+      const spec dsum = direct_importance_wave<LEAN, RRT_OCC_TAG(LEAN, WAVES), DCAP>(kp, g, cl, t, shade, dl[t >> 6]);
+      if (shade) s = emission(kp.bsdfs[lget(cl.bsdf, t)]) + dsum;
+    } else if (act && hit) {
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;

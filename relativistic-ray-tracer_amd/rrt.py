@@ -107,7 +107,9 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
            "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
-           "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy", "rrt_libm_eval"]
+           "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy", "rrt_libm_eval",
+           "rrt_set_proof_audit", "rrt_get_proof_audit"]
+AUDIT_KINDS = ("camera", "shadow", "pixel", "strip", "kerr")  # include/rrt.h RRT_AUDIT_*
 
 _lib = None
 
@@ -154,6 +156,9 @@ def lib():
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_launch_times.argtypes = [vp, C.c_uint32, vp, vp]
         L.rrt_libm_eval.argtypes = [vp, C.c_int, vp, vp, vp, C.c_uint64]
+        if hasattr(L, "rrt_set_proof_audit"):  # absent from older builds loaded through RRT_LIB
+            L.rrt_set_proof_audit.argtypes = [vp, C.c_int]
+            L.rrt_get_proof_audit.argtypes = [vp, vp]
         L.rrt_proof_envelope.argtypes = [vp]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
         for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_search_tree", 3),
@@ -423,6 +428,17 @@ class Renderer:
         s = Stats()
         self._chk(lib().rrt_get_stats(self.h, C.byref(s)))
         return s
+
+    def set_proof_audit(self, every_log2):
+        """Counting launches (RRT_RENDER_COUNTERS | RRT_RENDER_COUNT_EXECUTED) re-march every
+        2^every_log2-th proven ray exactly (rrt_set_proof_audit); every_log2 < 0 turns it off."""
+        self._chk(lib().rrt_set_proof_audit(self.h, every_log2))
+
+    def proof_audit(self):
+        """{proof: {"checked": n, "violations": m}} since the last call (rrt_get_proof_audit; resets)."""
+        out = np.zeros(2 * len(AUDIT_KINDS), np.uint64)
+        self._chk(lib().rrt_get_proof_audit(self.h, _p(out)))
+        return {k: {"checked": int(out[2 * i]), "violations": int(out[2 * i + 1])} for i, k in enumerate(AUDIT_KINDS)}
 
     def launch_times(self, n):
         """HIP-event ms of the last n (<= 32) launches, oldest first: (whole launch, main kernel)."""

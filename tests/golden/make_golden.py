@@ -71,6 +71,11 @@ CASES = {
     "cfg4_knot_4k_s256_crop2": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1920", "990", "64", "64"], False),
     "cfg4_knot_4k_s256_crop3": ("@cfg4", ["-s", "256", "-r", "3840", "2160", "-p", "1880", "1180", "64", "64"], False),
     "cfg4_knot_240x135_s16": ("@cfg4", ["-s", "16", "-r", "240", "135"], True),
+    # m3 (bench.py --workload m3: depth-3 bounce paths at the 1080p / 64 spp framing): two cells
+    "m3_spheres_1080p_s64_crop": ("CBspheres_lambertian.dae", ["-s", "64", "-m", "3", "-r", "1920", "1080",
+                                                               "-p", "928", "508", "64", "64"], False),
+    "m3_spheres_1080p_s64_crop2": ("CBspheres_lambertian.dae", ["-s", "64", "-m", "3", "-r", "1920", "1080",
+                                                                "-p", "1120", "360", "64", "64"], False),
     # cfg5 (BASELINE configs[4]) lighting: the generated HDR sky (rrt_scenes.sky_texels, "-e @sky"):
     # miss radiance of the unbent camera ray + importance-sampled environment light.  The
     # reference has no Kerr metric, so these pin the environment map under Schwarzschild.

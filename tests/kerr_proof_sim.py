@@ -20,6 +20,7 @@ STRETCH = 4.0    # RRT_KPROOF_STRETCH
 NEAR_M = 6.0     # RRT_KPROOF_NEAR_M
 DELTA_M = 0.25   # RRT_KPROOF_DELTA_M
 DT_MIN, DT_MAX, SPIN_MAX, REACH_M = 0.02, 0.1, 0.99, 40.0
+CENTRE_LO, CENTRE_HI, RS_LO, RS_HI = 0.2, 0.8, 0.04, 0.15  # the swept holes (tools/kerr_proof_sweep.py)
 
 
 def steps_of(dt):
@@ -40,7 +41,10 @@ def constants(bh, lo, hi, w):
     K = dict(c=c, m=m, dt=dt, lo=lo, hi=hi, stretch=STRETCH, r_near2=(NEAR_M * m) ** 2, delta=DELTA_M * m,
              swept_max=2.0 * np.pi - 0.5, max_steps=int((4 * steps_of(dt) - 2) / (1.25 * STRETCH)), r_esc2=r_esc2)
     K["box"] = (lo + w[:3] + 2.0 * K["delta"], hi - w[3:] - 2.0 * K["delta"])
-    K["in_envelope"] = DT_MIN <= dt <= DT_MAX and r_esc2 <= (REACH_M * m) ** 2
+    ext = hi - lo
+    inside = bool(np.all(c >= lo + CENTRE_LO * ext) and np.all(c <= lo + CENTRE_HI * ext))
+    rs_ok = RS_LO * ext.max() <= float(bh[3]) <= RS_HI * ext.max()
+    K["in_envelope"] = DT_MIN <= dt <= DT_MAX and r_esc2 <= (REACH_M * m) ** 2 and inside and rs_ok
     return K
 
 

@@ -30,6 +30,7 @@ def prove(K, O, dc, corners):
     Yc = Yc / dyc
     dlo = dhi = dxc
     dY = dd = 0.0
+    dymin = dyc
     for d in corners:
         dx = d @ X
         dlo, dhi = min(dlo, dx), max(dhi, dx)
@@ -37,8 +38,11 @@ def prove(K, O, dc, corners):
         dy = np.sqrt(yv @ yv)
         if not dy > 1e-3:
             return False
+        dymin = min(dymin, dy)
         dY = max(dY, np.linalg.norm(yv / dy - Yc))
         dd = max(dd, np.linalg.norm(d - dc))
+    if not dd <= 0.25 * dymin:  # +-X (where y turns round) kept well outside the rectangle
+        return False
     slack = 2.0 * dd * dd + 1e-12
     wdx = dhi - dlo
     dlo -= 0.05 * wdx + slack

@@ -22,7 +22,22 @@ def test_exports_match_header():
     L = rrt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rrt_abi_version() == 3
+    assert L.rrt_abi_version() == 4
+
+
+def test_proof_audit_needs_a_device():
+    """rrt_set_proof_audit: a host-only context cannot audit (no renders); off (< 0) is always
+    accepted; the tallies of a context that never audited are zero."""
+    r = rrt.Renderer(device=-1)
+    with pytest.raises(rrt.RRTError) as e:
+        r.set_proof_audit(10)
+    assert e.value.code == rrt.RRT_E_NO_DEVICE
+    with pytest.raises(rrt.RRTError) as e:
+        r.set_proof_audit(31)
+    assert e.value.code == rrt.RRT_E_INVALID
+    r.set_proof_audit(-1)
+    assert all(v == {"checked": 0, "violations": 0} for v in r.proof_audit().values())
+    r.close()
 
 
 @pytest.fixture(scope="module")

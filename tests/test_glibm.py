@@ -23,10 +23,37 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "relativistic-ray-tracer_amd", "csrc")
 
 
+def precondition():
+    """The parity precondition of rrt_glibm.h: the reference's bits are those of one
+    libm build (Ubuntu GLIBC 2.35, sha-pinned by tools/gen_glibm_tables.py) on an x86-64 CPU with FMA
+    and AVX2 (glibc's ifuncs then pick the FMA builds restated here).  None if it holds, else why not."""
+    import hashlib
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen", os.path.join(ROOT, "tools", "gen_glibm_tables.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    if not os.path.exists(gen.LIBM):
+        return f"no {gen.LIBM}"
+    with open(gen.LIBM, "rb") as f:
+        if hashlib.sha256(f.read()).hexdigest() != gen.LIBM_SHA256:
+            return "this host's libm is not the pinned build " + gen.EXPECTED
+    try:
+        with open("/proc/cpuinfo") as f:
+            flags = next((ln.split(":", 1)[1].split() for ln in f if ln.startswith("flags")), [])
+    except OSError:
+        flags = []
+    if not ({"fma", "avx2"} <= set(flags)):
+        return "the host CPU lacks FMA/AVX2: glibc would select other (non-FMA) builds"
+    return None
+
+
 @pytest.fixture(scope="module")
 def checker(tmp_path_factory):
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
+    why = precondition()
+    if why:
+        pytest.skip("PARITY PRECONDITION NOT MET (rrt_glibm.h restates one glibc build on FMA hosts): " + why)
     exe = str(tmp_path_factory.mktemp("glibm") / "glibm_check")
     subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fopenmp", "-I", CSRC,
                     os.path.join(ROOT, "tests", "glibm_check.c"), "-o", exe, "-lm"], check=True)

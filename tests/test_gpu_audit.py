@@ -1,0 +1,79 @@
+"""The run-time proof audit (include/rrt.h rrt_set_proof_audit).
+
+The renderer skips marches whose results its proofs determine -- the camera-ray miss proof, the
+shadow-ray occlusion proof, the pixel pass's pixel and strip proofs, the Kerr occlusion proof --
+with margins validated by sweeps.  A counting launch with the audit set re-marches proven rays
+exactly: here every one of them (every_log2 = 0) on frames whose proofs all fire, and no proof may
+be contradicted.  The audit must not change the frame."""
+import numpy as np
+import pytest
+
+import rrt
+from golden_cases import Case
+
+pytestmark = pytest.mark.gpu
+COUNT_X = rrt.RRT_RENDER_COUNTERS | rrt.RRT_RENDER_COUNT_EXECUTED
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    r = rrt.Renderer(device=0)
+    yield r
+    r.close()
+
+
+def _setup(gpu, c, spin=None, axis=(0.0, 1.0, 0.0), bh=None):
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(c.envmap)
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    b = bh or c.cfg["bh"]
+    gpu.set_black_hole(b[:3], b[3], b[4], spin=spin, axis=axis)
+
+
+def _params(c, flags):
+    g = c.cfg
+    return rrt.render_params(c.frame_w, c.frame_h, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"],
+                             ns_area_light=g["ns_area_light"], samples_per_batch=g["samples_per_batch"],
+                             max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=flags)
+
+
+@pytest.mark.parametrize("name", ["bunny_160x120_s16", "bunny_B1_160x120_s16", "spheres_B2_160x120_s16",
+                                  "cfg4_knot_240x135_s16", "empty_64x48_s8"])
+def test_audit_schwarzschild_proofs(gpu, name):
+    c = Case(name)
+    _setup(gpu, c)
+    p = _params(c, COUNT_X)
+    gpu.set_proof_audit(-1)
+    a0 = gpu.render(p, 0, 0, c.frame_w, c.frame_h, counters=True)
+    gpu.set_proof_audit(0)   # every proven ray and pixel
+    a1 = gpu.render(p, 0, 0, c.frame_w, c.frame_h, counters=True)
+    gpu.set_proof_audit(-1)
+    t = gpu.proof_audit()
+    print(name, t)
+    assert np.array_equal(a0[0].view(np.uint32), a1[0].view(np.uint32)) and np.array_equal(a0[1], a1[1])
+    assert np.array_equal(a0[0].view(np.uint32), c.px["rgb"].view(np.uint32))  # the reference's frame
+    assert t["camera"]["checked"] > 0 and t["pixel"]["checked"] > 0
+    assert all(v["violations"] == 0 for v in t.values()), t
+
+
+def test_audit_kerr_proof(gpu):
+    c = Case("bunny_160x120_s16")
+    _setup(gpu, c, spin=0.9)
+    gpu.set_proof_audit(0)
+    gpu.render(_params(c, COUNT_X), 0, 0, c.frame_w, c.frame_h, counters=True)
+    gpu.set_proof_audit(-1)
+    t = gpu.proof_audit()
+    print(t)
+    assert t["kerr"]["checked"] > 0 and t["kerr"]["violations"] == 0, t
+    assert t["camera"]["checked"] == 0  # Kerr has no camera proof
+
+
+def test_audit_off_outside_counting(gpu):
+    """Only counting launches audit: a plain render leaves the tallies at zero."""
+    c = Case("bunny_160x120_s16")
+    _setup(gpu, c)
+    gpu.set_proof_audit(0)
+    gpu.render(_params(c, 0), 0, 0, c.frame_w, c.frame_h)
+    gpu.set_proof_audit(-1)
+    t = gpu.proof_audit()
+    assert all(v["checked"] == 0 for v in t.values()), t

@@ -154,3 +154,40 @@ def test_kerr_a_to_0_limit_on_cfg5_framing(gpu, name, sub):
     ref = c.px["rgb"][y0 - c.y0:y0 - c.y0 + h, x0 - c.x0:x0 - c.x0 + w].astype(np.float64)
     print(name, "Kerr a=0 mean", rgb0.mean(axis=(0, 1)), "reference (Schwarzschild stepper) mean", ref.mean(axis=(0, 1)),
           "samples", int(cnt0.sum()), "vs", int(c.px["count"][y0 - c.y0:y0 - c.y0 + h, x0 - c.x0:x0 - c.x0 + w].sum()))
+
+
+def _random_kerr_holes(n, seed):
+    """Holes drawn inside the Kerr occlusion proof's envelope (rrt_host.cpp RRT_KPROOF_*: centre in
+    the middle 60% of CBbunny's root box [-1, 1] x [0, 1.5] x [-1, 1], r_s 0.08..0.3, delta_theta
+    0.02..0.1), random spins and axes."""
+    g = np.random.default_rng(seed)
+    lo, ext = np.array([-1.0, 0.0, -1.0]), np.array([2.0, 1.5, 2.0])
+    out = []
+    for _ in range(n):
+        c = lo + ext * (0.22 + 0.56 * g.random(3))
+        ax = g.normal(size=3)
+        out.append(((float(c[0]), float(c[1]), float(c[2])), float(g.choice([0.08, 0.12, 0.2, 0.28])),
+                    float(g.choice([0.03, 0.05, 0.1])), float(g.choice([0.3, 0.7, 0.95])),
+                    tuple(float(x) for x in ax / np.linalg.norm(ax))))
+    return out
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_kerr_proof_random_holes_bit_identical(gpu, k):
+    """Run-time audit of the Kerr occlusion proof away from cfg5's hole: random holes
+    inside its envelope, the frame with the proof (default) and with RRT_RENDER_NO_SHADOW_PROOF (every
+    shadow ray marched exactly) are bit-identical -- a false "occluded" would darken a lit sample."""
+    c = Case("bunny_160x120_s16")
+    ctr, rs, dt, spin, axis = _random_kerr_holes(4, 2025)[k]
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(None)
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    gpu.set_black_hole(ctr, rs, dt, spin=spin, axis=axis)
+    p0 = rrt.render_params(c.frame_w, c.frame_h, ns_aa=16)
+    p1 = rrt.render_params(c.frame_w, c.frame_h, ns_aa=16, flags=rrt.RRT_RENDER_NO_SHADOW_PROOF)
+    a = gpu.render(p0, 0, 0, c.frame_w, c.frame_h, draws=True)
+    b = gpu.render(p1, 0, 0, c.frame_w, c.frame_h, draws=True)
+    print(k, ctr, rs, dt, spin, "mean", float(a[0].mean()), "lit", float((a[0].sum(-1) > 0).mean()))
+    assert float(a[0].max()) > 0
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])

@@ -73,7 +73,8 @@ def test_switch_matches_restatement(gpu, name, over, osw, flags):
 
 
 def test_switches_rejected_where_not_built(gpu):
-    """Kerr has no switch build, and ILLUM 3 at depth 0 recurses without end in the reference."""
+    """Kerr has no switch build, and ILLUM 3 at depth 0 is rejected: the reference's recursion depth is
+    unbounded there (size_t Ray::depth wraps; only Russian roulette ends it), beyond RRT_MAX_DEPTH."""
     c = Case("spheres_96x72_s1")
     gpu.set_scene(rrt.SceneFile(c.scene_path))
     gpu.set_envmap(None)

@@ -42,6 +42,19 @@ def test_envelope_constants_match_the_library():
     assert K.DELTA_M == _hdr("RRT_KPROOF_DELTA_M") and K.DT_MIN == _hdr("RRT_KPROOF_DT_MIN")
     assert K.DT_MAX == _hdr("RRT_KPROOF_DT_MAX") and K.SPIN_MAX == _hdr("RRT_KPROOF_SPIN_MAX")
     assert K.REACH_M == _hdr("RRT_KPROOF_REACH_M")
+    assert K.CENTRE_LO == _hdr("RRT_KPROOF_CENTRE_LO") and K.CENTRE_HI == _hdr("RRT_KPROOF_CENTRE_HI")
+    assert K.RS_LO == _hdr("RRT_KPROOF_RS_LO") and K.RS_HI == _hdr("RRT_KPROOF_RS_HI")
+
+
+def test_envelope_excludes_unswept_holes():
+    """Holes outside the swept region (centre near a wall or outside the room, r_s outside the swept
+    range) get no proof."""
+    lo, hi, w = np.array([-1.0, 0.0, -1.0]), np.array([1.0, 1.5, 1.0]), np.zeros(6)
+    assert constants((0.0, 1.0, 0.0, 0.1, 0.1), lo, hi, w)["in_envelope"]
+    assert not constants((0.0, 1.45, 0.0, 0.1, 0.1), lo, hi, w)["in_envelope"]   # near the ceiling
+    assert not constants((0.0, 1.0, 3.0, 0.1, 0.1), lo, hi, w)["in_envelope"]    # outside the room
+    assert not constants((0.0, 1.0, 0.0, 0.05, 0.1), lo, hi, w)["in_envelope"]   # r_s below the sweep's
+    assert not constants((0.0, 1.0, 0.0, 0.4, 0.1), lo, hi, w)["in_envelope"]    # and above
 
 
 def test_small_envelope_sweep_sound():

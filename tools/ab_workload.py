@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B kernel variants (rrt_render_params.variant = waves per SIMD, flags) on a bench.py workload,
 interleaved rounds in one process; prints the HIP-event kernel time per variant.
-Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT or VARIANT:FLAGS)
+Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT, VARIANT:FLAGS or
+VARIANT:FLAGS:RRT_AB_X=V,... -- library A/B switches the launch reads from the environment)
 --world N: time each of the N ranks' tile sets (bench.py's block-cyclic split) on this one GPU and
 report the slowest rank per variant (the N-GPU frame's kernel time, without the gather)."""
 import argparse
@@ -53,7 +54,14 @@ def main():
     per_rank = {v: [[] for _ in sets] for v in a.variants}
     for _ in range(a.rounds):
         for v in a.variants:
-            var, _, fl = v.partition(":")
+            var, _, rest = v.partition(":")
+            fl, _, envs = rest.partition(":")  # VARIANT:FLAGS:NAME=VALUE,... (library A/B switches read per launch)
+            for kv in os.environ.copy():
+                if kv.startswith("RRT_AB_"):
+                    del os.environ[kv]
+            for kv in filter(None, envs.split(",")):
+                k, _, val = kv.partition("=")
+                os.environ[k] = val
             p = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), variant=int(var), flags=int(fl or 0))
             worst, tot_rgb, tot_cnt = 0.0, 0.0, 0
             for k, tiles in enumerate(sets):
@@ -68,7 +76,8 @@ def main():
             times[v].append(worst)
             sums[v] = (tot_rgb, tot_cnt)
             print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
-    same = len(set(s for v, s in sums.items() if ":" not in v)) <= 1  # diagnostic flags change outputs
+    # diagnostic flags change outputs; environment switches (third field) do not
+    same = len(set(s for v, s in sums.items() if v.split(":")[1:2] in ([], ["0"], [""]))) <= 1
     print(json.dumps({"workload": a.workload, "identical_outputs": same,
                       "median_ms": {v: float(np.median(t)) for v, t in times.items()},
                       **({"world": a.world, "rank_median_ms": {v: [float(np.median(x)) for x in pr] for v, pr in per_rank.items()}}

@@ -3,7 +3,10 @@
 mirror tests/pixel_proof_sim.py): random 8x8-aligned strips of a BASELINE framing; every pixel of
 every proven strip -- its four corners and two random jitters -- is marched by the oracle
 (ro_micro_chain, bit-exact with the reference), and no segment of it may come near the root box
-(a violation otherwise).  Usage: python3 tools/strip_proof_sweep.py --case cfg3_bunny_1080p_s64 --strips 2000"""
+(a violation otherwise).  Usage: python3 tools/strip_proof_sweep.py --case cfg3_bunny_1080p_s64 --strips 2000
+--fov H: the case's camera with a horizontal field of view of H degrees (vertical from the frame's
+aspect), to sweep wide-angle framings; small frames (e.g. --case spheres_96x72_s8) make strips that
+subtend large angles."""
 import argparse
 import ctypes as C
 import json
@@ -29,6 +32,7 @@ def main():
     ap.add_argument("--strips", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fov", type=float, default=None, help="override hFov (degrees)")
     a = ap.parse_args()
     c = Case(a.case)
     bh = np.array(c.cfg["bh"], np.float64)
@@ -43,10 +47,14 @@ def main():
     pos = np.array(cam.pos, np.float64)
     W, H = c.frame_w, c.frame_h
     mn, mx = C.c_double(), C.c_double()
+    hfov, vfov = cam.hFov, cam.vFov
+    if a.fov is not None:
+        hfov = a.fov
+        vfov = 2.0 * np.degrees(np.arctan(np.tan(np.radians(hfov) / 2.0) * H / W))
 
     def ray(sx, sy):
         o, d = np.zeros(3), np.zeros(3)
-        O.lib().ro_camera_ray(cam.hFov, cam.vFov, pos, cols, cam.nClip, cam.fClip, sx / W, sy / H, o, d,
+        O.lib().ro_camera_ray(hfov, vfov, pos, cols, cam.nClip, cam.fClip, sx / W, sy / H, o, d,
                               C.byref(mn), C.byref(mx))
         return o, d
 
@@ -68,7 +76,7 @@ def main():
                     k = O.lib().ro_micro_chain(bh, o2, d2, out, K["steps"] + 1)
                     rays += 1
                     viol += int(_loose_root_hit(lo, hi, out[:k]).any())
-    rec = dict(case=a.case, strips=a.strips, proven=proven, rays_checked=rays, violations=viol)
+    rec = dict(case=a.case, hfov=hfov, strips=a.strips, proven=proven, rays_checked=rays, violations=viol)
     print(json.dumps(rec))
     if a.out:
         json.dump(rec, open(a.out, "w"), indent=1)
