@@ -1159,6 +1159,22 @@ int ro_shadow_query(const ro_scene* s, const ro_params* p, const double* o, cons
   isect_t is; memset(&is, 0, sizeof(is));
   return bvh_intersect(&q, V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), &is);
 }
+/* The closest-hit query (BVHAccel::intersect with an Intersection, bvh.cpp:103-113) of one ray:
+ * returns hit (0/1) and out[0..2] hit_p, out[3..5] n, out[6] bsdf (test infrastructure: the camera
+ * hit proof's checks, tests/hit_proof_sim.py) */
+int ro_query(const ro_scene* s, const ro_params* p, const double* o, const double* d, double* out) {
+  rng_t g; memset(&g, 0, sizeof(g));
+  qctx q; q.s = s; q.g = &g;
+  if (p->bh_kind == 1) {
+    hole_init_kerr(&q.hole, p->bh_center, p->bh_radius, p->bh_dtheta, p->bh_spin, p->bh_axis);
+    kerr_set_escape(&q.hole, s->nodes[0].mn, s->nodes[0].mx);
+  } else hole_init(&q.hole, p->bh_center, p->bh_radius, p->bh_dtheta);
+  isect_t is; memset(&is, 0, sizeof(is));
+  const int hit = bvh_intersect(&q, V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), &is);
+  out[0] = is.hit_p.x; out[1] = is.hit_p.y; out[2] = is.hit_p.z;
+  out[3] = is.n.x; out[4] = is.n.y; out[5] = is.n.z; out[6] = is.bsdf;
+  return hit;
+}
 int ro_micro_chain(const double* bh, const double* o, const double* d, double* out, int max_rows) {
   hole_t h; hole_init(&h, bh, bh[3], bh[4]);
   ray_t m; m.o = V(o[0], o[1], o[2]); m.d = V(d[0], d[1], d[2]); m.min_t = 0; m.max_t = 0;

@@ -80,6 +80,7 @@ int ro_micro_chain(const double* bh /*cx,cy,cz,r,dtheta*/, const double* o, cons
 int ro_kerr_chain_st(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame,
                      double st, double* extra);
 int ro_shadow_query(const ro_scene* s, const ro_params* p, const double* o, const double* d);
+int ro_query(const ro_scene* s, const ro_params* p, const double* o, const double* d, double* out /*7*/);
 int ro_kerr_chain(const double* bh, const double* o, const double* d, double* out, int max_rows, double* frame);
 int ro_bbox_intersect(const double* mn, const double* mx, const double* o, const double* d, double min_t,
                       double max_t, double* t0, double* t1);

@@ -1039,8 +1039,10 @@ __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 
 // The whole march by the recurrence, step 0 included: the ray (o, d) is the state of a step from
 // the point A = o itself (|A - c| = 1 / u, so v_prev = rho u, E_prev = x, s_prev chosen so the
 // update yields s = u and the reference's u' = -u (d . x) / |d - (d . x) x|).
+// ms: margin scale (1; the zero-sample proof, whose ray starts at the camera hit proof's crossing
+// point rather than at the reference's hit point, takes RRT_ZERO_MS)
 template <int W = 0>
-__device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v3 d, int steps) {
+__device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v3 d, int steps, double ms = 1.0) {
 #pragma clang fp contract(fast)
   const DMissProof& mp = kp.miss;
   const DShadowProof& sp = kp.occ;
@@ -1075,7 +1077,7 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
     sig *= sg;
     const double av = fabs(v), avp = fabs(vprev);
     const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);  // |B - c| (upper bound)
-    const double m = mp.eta * (fmax(rp, r) + mp.scale);
+    const double m = (ms * mp.eta) * (fmax(rp, r) + mp.scale);
     // the segment must clear the capture sphere: its distance from the hole > r_s + m (the
     // camera proof's scalar distance: foot of the perpendicular inside, else the nearer end)
     const double rb = rc + m;
@@ -1095,6 +1097,134 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
       if (res) return res > 0;
     }
     a_in = b_in;
+    rp = r; vprev = v; ea = na; eb = nb;
+  }
+  return false;
+}
+
+// ------------------------------------------------------------------ camera-ray hit proof
+// ("zero samples").  91% of the cfg3 camera rays that reach the room first hit one of
+// the room's face triangles (walls, floor, ceiling: the occlusion proof's table), and from there
+// nearly every light sample's shadow ray is occluded, so the sample's radiance is +0 -- yet each such
+// sample marched its camera ray exactly (~12 micro steps and walks).  The proof marches the shadow
+// proof's recurrence from the camera ray itself and accepts "the reference's query hits kept face
+// triangle T, not a light, at a point within the recurrence's deviation of Q" when, at the shadow
+// proof's margin m for every segment up to the crossing:
+//   * the segment clears the capture sphere (a capture would end the query first, with no hit);
+//   * it clears the box holding every primitive but the kept face triangles (kp.occ.nocc_*);
+//   * every kept triangle of a face an end of it is past is certainly untouched (ends more than m on
+//     one side of its plane, or its plane crossing mq outside an edge) -- but one, T, which the
+//     segment certainly crosses (ends more than m on either side, the crossing point mq inside
+//     every edge).  Triangles of faces no end is past lie beyond the trigger box: untouched.
+// The reference's segments are within the recurrence's deviation (a small fraction of m) of these,
+// so its query reaches T's segment uncaptured, no primitive before it is hit, and T's test accepts:
+// its hit is T, at a point within that deviation of Q.  Anything else -- an uncertain triangle, two
+// crossings in one segment, a light, the ray leaving the room -- is no proof.
+// occ_touch: 2 = certain crossing (at q), 0 = certainly untouched, 1 = uncertain (NaN: 1)
+__device__ __forceinline__ int occ_touch(const DOccluder& t, v3 a, v3 b, double m, v3& q) {
+#pragma clang fp contract(fast)
+  const double da = t.n[0] * a.x + t.n[1] * a.y + t.n[2] * a.z - t.d;
+  const double db = t.n[0] * b.x + t.n[1] * b.y + t.n[2] * b.z - t.d;
+  if ((da > m && db > m) || (da < -m && db < -m)) return 0;
+  if (!((da > m && db < -m) || (da < -m && db > m))) return 1;
+  const double tq = da / (da - db);
+  q = V(a.x + (b.x - a.x) * tq, a.y + (b.y - a.y) * tq, a.z + (b.z - a.z) * tq);
+  const double mq = m * (2.0 + (fabs(b.x - a.x) + fabs(b.y - a.y) + fabs(b.z - a.z)) / fabs(da - db));
+  bool in = true, out = false;
+  for (int k = 0; k < 3; ++k) {
+    const double e = t.en[k][0] * q.x + t.en[k][1] * q.y + t.en[k][2] * q.z - t.eo[k];
+    in = in && e >= mq;
+    out = out || e <= -mq;
+  }
+  return in ? 2 : out ? 0 : 1;
+}
+// The kept triangles a segment with an end outside the trigger box may touch: -1 = no proof (an
+// uncertain one, or two crossings), else the number of certain crossings (0 or 1: face f, index i, q)
+__device__ __noinline__ int occ_first_cross(const KParams& kp, v3 a, v3 b, double m, int& fi, v3& q) {
+  const DShadowProof& sp = kp.occ;
+  int found = 0;
+#pragma unroll 1
+  for (int f = 0; f < 6; ++f) {
+    const int k = f < 3 ? f : f - 3;
+    const double ak = k == 0 ? a.x : k == 1 ? a.y : a.z, bk = k == 0 ? b.x : k == 1 ? b.y : b.z;
+    const bool past = f < 3 ? !(bk >= sp.in_lo[k] && ak >= sp.in_lo[k]) : !(bk <= sp.in_hi[k] && ak <= sp.in_hi[k]);
+    if (!past) continue;
+#pragma unroll 1
+    for (uint32_t i = 0; i < sp.n[f]; ++i) {
+      v3 qq;
+      const int r = occ_touch(sp.tri[f][i], a, b, m, qq);
+      if (r == 1 || (r == 2 && found)) return -1;
+      if (r == 2) { found = 1; fi = 4 * f + (int)i; q = qq; }
+    }
+  }
+  return found;
+}
+__device__ __forceinline__ bool in_box(const double* lo, const double* hi, v3 p) {
+  return p.x >= lo[0] && p.x <= hi[0] && p.y >= lo[1] && p.y <= hi[1] && p.z >= lo[2] && p.z <= hi[2];
+}
+__device__ __forceinline__ bool seg_clear_of_box(v3 a, v3 b, const double* lo, const double* hi, double m);
+__device__ __forceinline__ bool camera_hit_proof(const KParams& kp, v3 o, v3 d, v3& Q) {
+#pragma clang fp contract(fast)
+  const DMissProof& mp = kp.miss;
+  const DShadowProof& sp = kp.occ;
+  const DHole& h = kp.hole;
+  const v3 c = V(h.c[0], h.c[1], h.c[2]);
+  const v3 x0 = o - c;
+  const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
+  const v3 X = vmul(x0, u0);
+  const double dx = dot(d, X);
+  v3 Y = d - smul(dx, X);
+  const double dy = sqrt(norm2(Y));
+  if (!(dy > 1e-3)) return false;  // towards the hole
+  Y = vmul(Y, 1.0 / dy);
+  const double up0 = -u0 * dx / dy;
+  double vprev = mp.rho * u0, s = u0 * mp.co1 - up0 * h.sin_dt * mp.inv_rho;
+  double ea = 1.0, eb = 0.0, sig = 1.0, rp = r0;
+  bool a_in = occ_inside(sp, o), a_room = in_box(mp.lo, mp.hi, o);
+  v3 pa = o;
+  const double si2 = h.sin_dt * h.sin_dt, rc = h.r * (1.0 + 1e-9);
+#pragma unroll 1
+  for (int j = 0; j < h.steps; ++j) {
+    const double sg = vprev < 0.0 ? -1.0 : 1.0;
+    const double up = (vprev * mp.co1 - mp.rho * s) * mp.inv_si;
+    s = fabs(vprev) * mp.inv_rho;
+    const double f1 = -s + mp.k15 * s * s;
+    const double u2 = s + up * (h.dt * 0.5);
+    const double f2 = -u2 + mp.k15 * u2 * u2;
+    const double u3 = u2 + f1 * mp.dt2_4;
+    const double f3 = -u3 + mp.k15 * u3 * u3;
+    const double v = s + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
+    if (!(fabs(v) >= mp.kappa * (s + fabs(up) * h.dt))) return false;  // cancelling step (or NaN)
+    const double a = sg * mp.co1, b = sig * mp.si1;
+    const double na = a * ea - b * eb, nb = a * eb + b * ea;
+    sig *= sg;
+    const double av = fabs(v), avp = fabs(vprev);
+    const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);
+    const double m = mp.eta * (fmax(rp, r) + mp.scale);
+    const double rb = rc + m;  // clear of the capture sphere
+    const double D = v * v + vprev * vprev - 2.0 * mp.co1 * avp * v;
+    const bool inside = v * (mp.co1 * avp - v) < 0.0 && avp * (avp - mp.co1 * v) > 0.0;
+    const bool clear = inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(v * v, vprev * vprev);
+    if (!clear) return false;
+    const double ib = mp.rho / v;
+    const v3 pb = V(c.x + (na * ib) * X.x + (nb * ib) * Y.x, c.y + (na * ib) * X.y + (nb * ib) * Y.y,
+                    c.z + (na * ib) * X.z + (nb * ib) * Y.z);
+    const bool b_in = occ_inside(sp, pb);
+    int fi = -1, found = 0;
+    v3 q = pb;
+    if (!(a_in && b_in)) {
+      found = occ_first_cross(kp, pa, pb, m, fi, q);
+      if (found < 0) return false;
+    }
+    if (!seg_clear_of_box(pa, pb, sp.nocc_lo, sp.nocc_hi, m)) return false;  // clear of every other primitive
+    if (found) {
+      if ((sp.emit[fi >> 2] >> (fi & 3)) & 1u) return false;  // a light: its hit is not black
+      Q = q;
+      return true;
+    }
+    const bool b_room = in_box(mp.lo, mp.hi, pb);
+    if (a_room && !b_room) return false;  // leaving the room without a crossing
+    a_in = b_in; a_room = b_room; pa = pb;
     rp = r; vprev = v; ea = na; eb = nb;
   }
   return false;

@@ -462,9 +462,10 @@ static void build_occluders(rrt_ctx* c) {
   for (int k = 0; k < 3; ++k) sc = std::max(sc, hi[k] - lo[k]);
   if (!(sc > 0.0) || !std::isfinite(sc)) return;
   const double tol = 1e-2 * sc;
-  struct Cand { double area, w; DOccluder t; V3 v[3]; };
+  struct Cand { double area, w; DOccluder t; V3 v[3]; uint32_t prim; };
   std::vector<Cand> cand[6];
-  for (const Prim& p : c->prims) {
+  for (uint32_t pi = 0; pi < (uint32_t)c->prims.size(); ++pi) {
+    const Prim& p = c->prims[pi];
     if (p.kind != RRT_OBJ_MESH) continue;
     const V3 p0 = c->pos[p.v[0]], e1 = sub(c->pos[p.v[1]], p0), e2 = sub(c->pos[p.v[2]], p0);
     const V3 q[3] = {p0, add(p0, e1), add(p0, e2)};
@@ -501,9 +502,10 @@ static void build_occluders(rrt_ctx* c) {
         const V3 v = q[(i + 2) % 3];
         ok = t.en[i][0] * v.x + t.en[i][1] * v.y + t.en[i][2] * v.z - t.eo[i] > 0.0;
       }
-      if (ok) cand[f].push_back({0.5 * nl, w, t, {q[0], q[1], q[2]}});
+      if (ok) cand[f].push_back({0.5 * nl, w, t, {q[0], q[1], q[2]}, pi});
     }
   }
+  std::vector<uint8_t> kept(c->prims.size(), 0);
   for (int f = 0; f < 6; ++f) {
     std::stable_sort(cand[f].begin(), cand[f].end(), [](const Cand& x, const Cand& y) { return x.area > y.area; });
     size_t keep = std::min<size_t>(cand[f].size(), RRT_OCC_PER_FACE);
@@ -512,6 +514,9 @@ static void build_occluders(rrt_ctx* c) {
     for (uint32_t i = 0; i < o.n[f]; ++i) {
       o.tri[f][i] = cand[f][i].t;
       o.w[f] = std::max(o.w[f], cand[f][i].w);
+      const uint32_t b = c->prims[cand[f][i].prim].bsdf;
+      if (b >= c->bsdfs.size() || c->bsdfs[b].type == RRT_BSDF_EMISSION) o.emit[f] |= 1u << i;  // a light
+      kept[cand[f][i].prim] = 1;
     }
     // The Kerr proof's wall pieces: two kept triangles that share an edge (vertices within 1e-9 of
     // the box's extent), lie in one plane and form a convex quad are one piece -- the crossing may
@@ -566,6 +571,13 @@ static void build_occluders(rrt_ctx* c) {
     }
     c->occ_nq[f] = nq;
   }
+  // The camera-ray hit proof (rrt_device.h camera_hit_proof): every primitive but the kept face
+  // triangles lies in this box (empty: lo > hi); a segment that clears it touches no such primitive
+  Box nb = Box::empty();
+  for (uint32_t pi = 0; pi < (uint32_t)c->prims.size(); ++pi)
+    if (!kept[pi]) nb.expand(prim_box(c, c->prims[pi]));
+  o.nocc_lo[0] = nb.mn.x; o.nocc_lo[1] = nb.mn.y; o.nocc_lo[2] = nb.mn.z;
+  o.nocc_hi[0] = nb.mx.x; o.nocc_hi[1] = nb.mx.y; o.nocc_hi[2] = nb.mx.z;
 }
 
 static void build_free_grid(rrt_ctx* c) {
@@ -1379,6 +1391,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // the point-light scenes' builds carry no proof (rrt_sample.hip RRT_OCC_TAG); off for them in
     // every kernel, so the counting passes count what their batch kernel executes
     kp.occ.on = (proofs_valid && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
+    // zero samples (rrt_sample.hip zero_sample_proof): the camera-ray hit proof plus the occlusion
+    // proof, for the area-light scenes (A/B and parity: RRT_AB_NO_ZERO=1 in the environment)
+    {
+      const char* nz = std::getenv("RRT_AB_NO_ZERO");
+      kp.occ.hit_on = (kp.occ.on && c->lean == 1 && !(nz && nz[0] == '1') && !(p->flags & RRT_RENDER_NO_MISS_PROOF)) ? 1u : 0u;
+    }
     // Kerr shadow rays (rrt_device.h kerr_occluded_proof): the same face triangles
     // against a coarse march, inside the envelope its margin was swept over
     // (tools/kerr_proof_sweep.py -> profiles/r04_kerr_proof_sweep.json)

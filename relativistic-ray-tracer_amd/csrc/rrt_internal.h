@@ -129,6 +129,12 @@ struct DShadowProof {
   double w[6];            // host: the kept triangles' largest vertex distance from their face
   uint32_t n[6];
   uint32_t on, pad;
+  // camera-ray hit proof (rrt_device.h camera_hit_proof): bit i of emit[f] = kept triangle i of face
+  // f is a light (a hit on it is not black); every other primitive of the scene lies in the box
+  // [nocc_lo, nocc_hi] (lo > hi: none); hit_on enables the proof (the area-light build)
+  uint32_t emit[6];
+  uint32_t hit_on, hit_pad;
+  double nocc_lo[3], nocc_hi[3];
 };
 
 // Kerr shadow-ray occlusion proof (rrt_device.h kerr_occluded_proof): a coarse march

@@ -111,6 +111,37 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 }
 
 // ---------------------------------------------------------------------------------------------
+// Zero samples.  A camera ray that camera_hit_proof shows to hit a non-emitting face
+// triangle of the room near Q, and whose every light sample's shadow ray from Q the occlusion proof
+// shows occluded, renders +0: emission 0 (est_radiance_global_illumination, part1_code.cpp:103-123)
+// plus direct light 0 -- an occluded sample adds nothing (part1_code.cpp:52-55), whatever its BSDF
+// value, pdf or cosine -- with the hit's draws (the light samples draw the same numbers from the
+// slot's stream).  Q lies within the recurrence's deviation (tools/hit_proof_sweep.py: < 2e-13) of the
+// reference's hit point, so the shadow proofs run with RRT_ZERO_MS times the margins.  The batch
+// kernel then skips the sample's exact camera march and its shading.  g: the slot's stream after
+// the jitter draws.
+#ifndef RRT_ZERO_MS
+#define RRT_ZERO_MS 2.0
+#endif
+#define RRT_ZERO_BSDF 0xffffffffu  // the parked record of a zero sample (no shading)
+template <int LEAN, int W>
+__device__ __forceinline__ bool zero_sample_proof(const KParams& kp, v3 o, v3 d, Rng g) {
+  v3 Q;
+  if (!camera_hit_proof(kp, o, d, Q)) return false;
+  if (kp.max_ray_depth == 0) return true;
+  for (uint32_t li = 0; li < kp.n_lights; ++li) {
+    const int num = kp.lights[li].is_delta ? 1 : (int)kp.ns_area_light;
+    for (int i = 0; i < num; ++i) {
+      v3 wi;
+      float dist, pdf;
+      (void)light_sample_L<LEAN>(kp.env, kp.lights[li], g, Q, wi, dist, pdf);
+      if (!shadow_occluded_proof<W>(kp, Q + smul(EPS_D, wi), wi, kp.hole.steps, RRT_ZERO_MS)) return false;
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Segment-parallel shadow queries ("dealt walks").  BVHAccel::intersect
 // (bvh.cpp:103-113) marches a chain of micro segments; each segment depends only on the one before
 // (BlackHole::next_micro_ray, blackhole.cpp:17-40), never on a walk's result, and a shadow query is
@@ -123,7 +154,13 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
 // ended) each lane of the wave walks one listed segment; a ray stops generating once one of its
 // walks has hit.  The answer is the reference's: hit <=> some uncaptured segment's walk hits.
 #ifndef RRT_DEAL
-#define RRT_DEAL 1  // 0: build without the dealt shadow walks (A/B)
+#define RRT_DEAL 0  // 1: build with the dealt shadow walks (A/B: slower, DESIGN.md §5 -- cfg3 15.45 ms without,
+                    // 16.56 ms with shadow_dealt inlined, 17.44 ms out of line; no gain on the 8-way split)
+#endif
+#ifndef RRT_ZERO
+#define RRT_ZERO 0  // 1: build with the zero samples in the batch kernel (A/B: slower, DESIGN.md §5 -- cfg3
+                    // 19.1-19.5 ms with, 15.5 ms without; the proof's registers raise the kernel's spills
+                    // 161 -> 272 VGPRs and its saved marches do not shorten the waves that run them)
 #endif
 #ifndef RRT_DEAL_CAP
 #define RRT_DEAL_CAP 32  // listed segments per wave (LDS: 60 B each)
@@ -163,13 +200,15 @@ __device__ RRT_DEAL_ATTR bool shadow_dealt(const KParams& kp, v3 o, v3 d, bool n
 #pragma unroll 1
   for (;;) {
     uint32_t n = 0;  // listed segments (wave-uniform)
-    // generate: every chain one micro step per pass, while the list has room for a segment of each
+    // generate: the chains one micro step per pass -- as many of them as the list has room for a
+    // segment of (the first generating lanes), the others wait for the next pass
 #pragma unroll 1
     for (;;) {
       const uint64_t gm = __ballot(gen);
-      if (gm == 0 || n + (uint32_t)__popcll(gm) > CAP) break;
+      if (gm == 0 || n == CAP) break;
+      const bool step = gen && (uint32_t)__popcll(gm & lt) < CAP - n;
       bool want = false;
-      if (gen) {
+      if (step) {
         v3 rel;
         double rel2;
         next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
@@ -414,11 +453,14 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
     const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     spec s = S(0, 0, 0);
+    const Rng g_jit = g;  // the stream after the jitter (the zero-sample audit's light samples)
     {
       Isect is;
       const v3 wd = unit(w);
+      bool hitq = false;
       if (!camera_proven_miss<COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
           query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
+        hitq = true;
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
         else if (DEEP && kp.max_ray_depth >= 2) s = e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
@@ -427,6 +469,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         else s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
       } else if (!is_lean(LEAN) && kp.env.w) {
         s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
+      }
+      // audit of the zero samples (the batch kernel's area-light build): a proven zero sample must be
+      // a hit whose radiance is +0 here, where it is marched and shaded exactly
+      if (COUNT && kp.audit && kp.occ.hit_on && LEAN != V_KERR && audit_pick(kp, ld3(cam.pos), wd) &&
+          zero_sample_proof<0, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, ld3(cam.pos), wd, g_jit)) {
+        const bool ok = hitq && s.r == 0.0f && s.g == 0.0f && s.b == 0.0f && !signbit(s.r) && !signbit(s.g) && !signbit(s.b);
+        audit_note(kp, RRT_AUDIT_ZERO, !ok);
       }
       if (COUNT && aud) {  // the pixel pass's proofs say this camera ray misses
         Counters c2 = {};
@@ -716,6 +765,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   // the area-light build at <= 4 waves/SIMD (LDS: 4 blocks of 28.5 + 7.7 KB a CU); not the point-light
   // build (no occlusion proof, few shadow rays: cfg4's frame is its camera rays)
   constexpr bool DEAL = RRT_DEAL && LEAN == 1 && WAVES <= 4;
+  constexpr bool ZERO = RRT_ZERO && LEAN == 1;  // zero samples (zero_sample_proof): the area-light build
   constexpr uint32_t DCAP = DEAL ? (uint32_t)RRT_DEAL_CAP : 1u;
   __shared__ DealLds<DCAP> dl[4];  // one per wave (shadow_dealt)
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
@@ -912,8 +962,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
       const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
       const v3 wd = unit(w);
-      return !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
-             query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, is, cn);
+      if (camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn)) return false;
+      if (ZERO && kp.occ.hit_on && zero_sample_proof<LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, ld3(cam.pos), wd, g)) {
+        is->bsdf = (int)RRT_ZERO_BSDF;  // a hit whose radiance is +0: no record, no shading
+        return true;
+      }
+      return query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, is, cn);
     };
     const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;  // this group's lanes
     const uint64_t lt = ((1ull << lane) - 1ull) & gmask;                         // group lanes before me
@@ -1038,13 +1092,14 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
       s = env_dir(kp.env, unit(w));
     }
+    const bool zero = ZERO && act && hit && lget(cl.bsdf, t) == RRT_ZERO_BSDF;  // radiance +0
     if (DEAL && kp.deal && kp.max_ray_depth != 0) {
       // every lane takes part: the unproven shadow rays' walks are dealt over the wave (shadow_dealt)
-      const bool shade = act && hit;
+      const bool shade = act && hit && !zero;
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec dsum = direct_importance_wave<LEAN, RRT_OCC_TAG(LEAN, WAVES), DCAP>(kp, g, cl, t, shade, dl[t >> 6]);
       if (shade) s = emission(kp.bsdfs[lget(cl.bsdf, t)]) + dsum;
-    } else if (act && hit) {
+    } else if (act && hit && !zero) {
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;

@@ -109,7 +109,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
            "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy", "rrt_libm_eval",
            "rrt_set_proof_audit", "rrt_get_proof_audit"]
-AUDIT_KINDS = ("camera", "shadow", "pixel", "strip", "kerr")  # include/rrt.h RRT_AUDIT_*
+AUDIT_KINDS = ("camera", "shadow", "pixel", "strip", "kerr", "zero")  # include/rrt.h RRT_AUDIT_*
 
 _lib = None
 

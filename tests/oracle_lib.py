@@ -62,6 +62,7 @@ def lib():
         L.ro_kerr_chain.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int, _f64p]
         L.ro_kerr_chain_st.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_int, _f64p, C.c_double, _f64p]
         L.ro_shadow_query.argtypes = [C.c_void_p, C.POINTER(Params), _f64p, _f64p]
+        L.ro_query.argtypes = [C.c_void_p, C.POINTER(Params), _f64p, _f64p, _f64p]
         L.ro_bbox_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.c_double, C.c_double,
                                         C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.ro_tri_intersect.argtypes = [_f64p, _f64p, _f64p, _f64p, C.POINTER(C.c_double), _f64p, _f64p]
@@ -167,6 +168,14 @@ def kerr_chain_st(bh, spin, axis, o, d, st, max_rows=64):
 def shadow_query(scene, params, o, d):
     """BVHAccel::intersect's boolean for the ray (o, d) under params' spacetime (restatement)."""
     return bool(lib().ro_shadow_query(scene.h, C.byref(params), np.asarray(o, np.float64), np.asarray(d, np.float64)))
+
+
+def query(scene, params, o, d):
+    """The reference's closest-hit query of one ray: (hit, hit_p [3], n [3], bsdf)."""
+    out = np.zeros(7)
+    h = lib().ro_query(scene.h, C.byref(params), np.ascontiguousarray(o, np.float64),
+                       np.ascontiguousarray(d, np.float64), out)
+    return bool(h), out[:3].copy(), out[3:6].copy(), int(out[6])
 
 
 def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):

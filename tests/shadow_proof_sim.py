@@ -98,7 +98,7 @@ def _exit(faces, box, K, a, b, m):
     return (-1 if out else 0), -1
 
 
-def run(K, faces, box, o, d):
+def run(K, faces, box, o, d, ms=1.0):
     """The proof for rays (o, d).  Returns (proven [n], step [n], triangle [n], points [steps+1, n, 3]
     of the recurrence (NaN once a ray's proof ended), margins [steps+1, n])."""
     n = len(o)
@@ -141,7 +141,7 @@ def run(K, faces, box, o, d):
             sig = sig * sg
             av, avp = np.abs(v), np.abs(vprev)
             r = K["rho"] / av * (1.0 + 1e-6)
-            m = ETA * (np.maximum(rp, r) + K["scale"])
+            m = ms * ETA * (np.maximum(rp, r) + K["scale"])
             rb = rc + m
             D = v * v + vprev * vprev - 2.0 * K["co1"] * avp * v
             inside = (v * (K["co1"] * avp - v) < 0.0) & (avp * (avp - K["co1"] * v) > 0.0)

@@ -37,22 +37,35 @@ def _params(c, flags):
                              max_tolerance=g["max_tolerance"], direct_hemisphere=g["direct_hemisphere"], flags=flags)
 
 
-@pytest.mark.parametrize("name", ["bunny_160x120_s16", "bunny_B1_160x120_s16", "spheres_B2_160x120_s16",
-                                  "cfg4_knot_240x135_s16", "empty_64x48_s8"])
-def test_audit_schwarzschild_proofs(gpu, name):
+# (case, region, whether the region holds proven camera rays / pixels: the small frames' narrow
+# fields of view see only the room, so there the shadow proof is what runs)
+AUDIT_CASES = [("cfg3_bunny_1080p_s64", (832, 412, 256, 256), False), ("cfg3_bunny_1080p_s64", (0, 0, 192, 192), True),
+               ("cfg2_spheres_1080p_s64_flat", (1600, 800, 128, 128), True), ("bunny_160x120_s16", None, False),
+               ("bunny_B1_160x120_s16", None, False), ("spheres_B2_160x120_s16", None, False),
+               ("cfg4_knot_240x135_s16", None, False), ("empty_64x48_s8", None, False)]
+
+
+@pytest.mark.parametrize("name,region,misses", AUDIT_CASES)
+def test_audit_schwarzschild_proofs(gpu, name, region, misses):
     c = Case(name)
     _setup(gpu, c)
     p = _params(c, COUNT_X)
+    x0, y0, w, h = region or (0, 0, c.frame_w, c.frame_h)
     gpu.set_proof_audit(-1)
-    a0 = gpu.render(p, 0, 0, c.frame_w, c.frame_h, counters=True)
+    a0 = gpu.render(p, x0, y0, w, h, counters=True)
     gpu.set_proof_audit(0)   # every proven ray and pixel
-    a1 = gpu.render(p, 0, 0, c.frame_w, c.frame_h, counters=True)
+    a1 = gpu.render(p, x0, y0, w, h, counters=True)
     gpu.set_proof_audit(-1)
     t = gpu.proof_audit()
-    print(name, t)
+    print(name, region, t)
     assert np.array_equal(a0[0].view(np.uint32), a1[0].view(np.uint32)) and np.array_equal(a0[1], a1[1])
-    assert np.array_equal(a0[0].view(np.uint32), c.px["rgb"].view(np.uint32))  # the reference's frame
-    assert t["camera"]["checked"] > 0 and t["pixel"]["checked"] > 0
+    ref = c.px["rgb"][y0 - c.y0:y0 - c.y0 + h, x0 - c.x0:x0 - c.x0 + w]
+    assert np.array_equal(a0[0].view(np.uint32), ref.view(np.uint32))  # the reference's frame
+    if misses:
+        assert t["camera"]["checked"] > 0 and t["pixel"]["checked"] > 0 and t["strip"]["checked"] > 0, t
+    if name.startswith("cfg3") and region[0] > 0:  # the room: zero samples (camera hit + occlusion proofs)
+        assert t["zero"]["checked"] > 0, t
+    assert sum(v["checked"] for v in t.values()) > 0, t
     assert all(v["violations"] == 0 for v in t.values()), t
 
 
