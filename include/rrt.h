@@ -360,6 +360,12 @@ int rrt_get_clean_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes, double
  * ordinal).  Returns n (0 = none); call with NULL pointers to get n. */
 int rrt_get_search_tree(const rrt_ctx* ctx, double* boxes, int32_t* nodes);
 
+/* The search tree 4 wide (the walk's 4-wide nodes): boxes [n][4][6] f32 (min, max;
+ * rounded outward and widened: a conservative pre-test), kids [n][4][3] = (child, first slot, count):
+ * count 0 an inner node (child = its 4-wide index), > 0 a search-tree leaf (child = its search-tree
+ * node index), < 0 empty.  Returns n (0 = none: the binary walk); any pointer may be NULL. */
+int rrt_get_search_tree4(const rrt_ctx* ctx, float* boxes, int32_t* kids);
+
 /* The empty-space grid: k [n[2]][n[1]][n[0]] uint8 Chebyshev cell distances,
  * geom = {g0.x, g0.y, g0.z, 1/h, h_free}.  Returns the number of cells (0 = no grid); any
  * pointer may be NULL.  For host-side tests of its conservativeness. */

@@ -504,6 +504,153 @@ __device__ __forceinline__ bool traverse_free(const KParams& kp, v3 o, v3 d, v3 
   return hit;
 }
 
+// traverse_free over the 4-wide search tree (kp.free4, rrt_host.cpp build_free4): the same leaves,
+// each tested with the same slab test at L, but four child boxes per node load -- a walk of a slow
+// pixel's micro segment is a chain of ~40 dependent box tests on the binary tree, ~10 node loads
+// here.  The collect order differs, which the collect pass allows (it keeps every
+// primitive accepted at L; the replay below is traverse_free's).  DFS stack: up to 8 node indices
+// of 16 bits in two registers; returns 2 when it would overflow (no result: the caller walks the
+// binary tree), else hit (1) or not (0).
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ int traverse_free4(const KParams& kp, v3 o, v3 d, v3 y, double& max_t, int& hit_slot,
+                                              double& hb1, double& hb2, Counters& cn, bool exact,
+                                              uint64_t bmask = ~0ull, bool any_rt = false) {
+  // the f32 pre-test's range: origins within free4_omax (else the binary walk)
+  if (!(fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= kp.free4_omax)) return 2;
+  if (COUNT) cn.bbox++;
+  if (!slab_rt(kp.nodes[0].mn, kp.nodes[0].mx, o, d, y, max_t, exact)) return 0;
+  bmask &= kp.free_big_mask;
+  const double L = max_t;
+  const v3 e = o + vmul(d, L);
+  const int nb = (int)kp.n_big;
+  bool hit = false;
+  double m = L;
+  int32_t after = -1, leaf_cut = 0x7fffffff;
+  bool cut_pass = false;
+  // the segment in f32 for the pre-test: origin rounded to nearest, reciprocals clamped finite,
+  // the length rounded up
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float ix = (float)fmin(fmax(y.x, -1e30), 1e30), iy = (float)fmin(fmax(y.y, -1e30), 1e30),
+              iz = (float)fmin(fmax(y.z, -1e30), 1e30);
+  const float Lf = (float)(L * (1.0 + 1e-6)) * 1.000001f;
+#pragma unroll 1
+  for (;;) {
+    int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+    int na = 0;
+    bool more = false;
+    // a leaf whose box passed at L: its primitives accepted at L into the window (traverse_free)
+    auto take = [&](int32_t first, int32_t count, int32_t ref) -> bool {  // true: a shadow query's hit
+#pragma unroll 1
+      for (int i = 0; i < count; ++i) {
+        const int32_t slot = first + i;
+        if (slot <= after) continue;
+        if (COUNT) cn.query++;
+        if (!plane_may_hit(kp.planes[slot], o, e, kp.plane_eps)) continue;
+        if (COUNT) cn.prim++;
+        const DPrimMeta meta = kp.meta[slot];
+        const DPrimGeo gp = kp.geo[slot];
+        double t, b1 = 0, b2 = 0;
+        const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, L, t)
+                                    : tri_t(gp, o, d, L, t, b1, b2);
+        if (!ok) continue;
+        if (ANY || any_rt) return true;
+        if (na == 4) {
+          more = true;
+          if (slot > s3) continue;
+          --na;
+        }
+        bool placed = false;
+        if (na >= 3) { if (s2 > slot) { s3 = s2; r3 = r2; } else { s3 = slot; r3 = ref; placed = true; } }
+        if (!placed && na >= 2) { if (s1 > slot) { s2 = s1; r2 = r1; } else { s2 = slot; r2 = ref; placed = true; } }
+        if (!placed && na >= 1) { if (s0 > slot) { s1 = s0; r1 = r0; } else { s1 = slot; r1 = ref; placed = true; } }
+        if (!placed) { s0 = slot; r0 = ref; }
+        ++na;
+      }
+      return false;
+    };
+    // the room-spanning oversized leaves (plane cull first)
+#pragma unroll 1
+    for (int bi = next_big_in(bmask, 0, nb); bi < nb; bi = next_big_in(bmask, bi + 1, nb)) {
+      const DBig& B = kp.big[bi];
+      if (!leaf_may_hit<COUNT>(kp, B.first, B.count, o, e, cn)) continue;
+      if (COUNT) cn.bbox++;
+      if (!slab_rt(B.mn, B.mx, o, d, y, L, exact)) continue;
+      if (take(B.first, B.count, -1 - bi)) return 1;
+    }
+    // the tree: the search tree's root box, then its nodes four children at a time
+    if (COUNT) cn.bbox++;
+    if (slab_rt(kp.free_nodes[0].mn, kp.free_nodes[0].mx, o, d, y, L, exact)) {
+      uint64_t st0 = 0, st1 = 0;
+      int sp = 0;
+      uint32_t cur = 0;
+#pragma unroll 1
+      for (;;) {
+        const DNode4& N = kp.free4[cur];
+        uint32_t pass = 0;
+        // the conservative f32 pre-test of the four children (widened boxes: never fails a box the
+        // exact test passes)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a0 = (N.mnx[i] - ox) * ix, a1 = (N.mxx[i] - ox) * ix;
+          const float b0 = (N.mny[i] - oy) * iy, b1 = (N.mxy[i] - oy) * iy;
+          const float c0 = (N.mnz[i] - oz) * iz, c1 = (N.mxz[i] - oz) * iz;
+          const float tmin = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fminf(c0, c1));
+          const float tmax = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1));
+          if (N.count[i] >= 0 && !(tmin > tmax || tmin > Lf || tmax < 0.0f)) pass |= 1u << i;
+        }
+#pragma unroll 1
+        while (pass) {
+          const int i = (int)__builtin_ctz(pass);
+          pass &= pass - 1;
+          if (N.count[i] > 0) {
+            // a leaf: the exact test on its own box (traverse_free's), then its primitives
+            const DNode& F = kp.free_nodes[N.child[i]];
+            if (COUNT) cn.bbox++;
+            if (!slab_rt(F.mn, F.mx, o, d, y, L, exact)) continue;
+            if (take(N.first[i], N.count[i], N.child[i])) return 1;
+          } else {
+            if (sp == 8) return 2;  // the stack is full: the caller walks the binary tree
+            st1 = (st1 << 16) | (st0 >> 48);
+            st0 = (st0 << 16) | (uint64_t)(uint32_t)N.child[i];
+            ++sp;
+          }
+        }
+        if (sp == 0) break;
+        cur = (uint32_t)(st0 & 0xffffull);
+        st0 = (st0 >> 16) | (st1 << 48);
+        st1 >>= 16;
+        --sp;
+      }
+    }
+    if (ANY || na == 0) break;
+    // ---- replay the reference on this window, in slot (= its visiting) order (traverse_free)
+    bool pass = false;
+    int32_t curr = 0x7fffffff;
+#pragma unroll 1
+    for (int k = 0; k < na; ++k) {
+      const int32_t slot = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+      const int32_t ref = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r3;
+      if (ref != curr) {
+        curr = ref;
+        const double* mn = ref >= 0 ? kp.free_nodes[ref].mn : kp.big[-1 - ref].mn;
+        const double* mx = ref >= 0 ? kp.free_nodes[ref].mx : kp.big[-1 - ref].mx;
+        pass = ref == leaf_cut ? cut_pass : slab_rt(mn, mx, o, d, y, m, exact);
+      }
+      if (!pass) continue;
+      const DPrimMeta meta = kp.meta[slot];
+      const DPrimGeo gp = kp.geo[slot];
+      double t, b1 = 0, b2 = 0;
+      const bool ok = (meta & 1u) ? sphere_t(V(gp.v[0], gp.v[1], gp.v[2]), gp.v[3], o, d, m, t)
+                                  : tri_t(gp, o, d, m, t, b1, b2);
+      if (ok) { m = t; hit = true; hit_slot = slot; hb1 = b1; hb2 = b2; }
+    }
+    if (!more) break;
+    after = s3; leaf_cut = r3; cut_pass = pass;
+  }
+  max_t = m;
+  return hit ? 1 : 0;
+}
+
 // BlackHole::next_micro_ray (blackhole.cpp:17-40); f4 is computed but unused there.  Each norm
 // is computed once and its reciprocal shared: normalize(v) = v * (1 / norm(v)) (vector3D.h), and
 // u = 1 / |x| is that same reciprocal -- the same values as evaluating them separately, at half
@@ -616,10 +763,13 @@ __device__ __forceinline__ bool segment_walk(const KParams& kp, v3 o, v3 d, doub
   const bool fast = segment_fast(kp, o, d);
   RRT_T0(tt0);
   bool hit;
-  if (!COUNT)  // the search tree (or, for A/B, the clean tree or the reference tree itself)
-    hit = traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt);
-  else if (kp.count_exec)
-    hit = traverse_free<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask);
+  if (!COUNT) {  // the search tree (4 wide, else binary; or, for A/B, the clean tree or the reference tree)
+    const int r4 = kp.free4 ? traverse_free4<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt) : 2;
+    hit = r4 == 2 ? traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt) : r4 == 1;
+  } else if (kp.count_exec) {
+    const int r4 = kp.free4 ? traverse_free4<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask) : 2;
+    hit = r4 == 2 ? traverse_free<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask) : r4 == 1;
+  }
   else
     hit = fast ? traverse<ANY, COUNT, false>(kp, o, d, y, seg_t, slot, b1, b2, cn)
                : traverse<ANY, COUNT, true>(kp, o, d, y, seg_t, slot, b1, b2, cn);
@@ -1242,8 +1392,11 @@ __device__ __forceinline__ bool camera_hit_proof(const KParams& kp, v3 o, v3 d, 
 #ifndef RRT_QUERY_AHEAD
 #define RRT_QUERY_AHEAD 0  // 1: lanes skip ahead to their next walk (A/B; slower, profiles/r04_ab_query_ahead.txt)
 #endif
-#ifndef RRT_QUERY_ATTR  // a translation unit may force the query inline (rrt_path.hip)
-#define RRT_QUERY_ATTR __device__
+#ifndef RRT_QUERY_ATTR  // inline into every kernel build: a query shared out of line by builds of
+                        // different waves-per-SIMD budgets takes the loosest budget's registers, and
+                        // every caller inherits them (occupancy 4 -> 1 when the 4-wide walk made the
+                        // query too large for the inliner)
+#define RRT_QUERY_ATTR __device__ __forceinline__
 #endif
 template <bool ANY, bool COUNT, bool KERR = false>
 RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn, bool any_rt = false) {

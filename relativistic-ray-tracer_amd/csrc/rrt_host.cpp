@@ -186,6 +186,9 @@ struct rrt_ctx {
   std::vector<DBig> big;
   std::vector<uint32_t> big_mask;   // build_big_masks (host copy; rrt_get_big_masks)
   std::vector<DNode> free_tree;     // build_free_tree: SAH hierarchy over the clean tree's leaves
+  std::vector<DNode4> free4;        // build_free4: the same hierarchy 4 wide (empty: none)
+  DNode4* d_free4 = nullptr;
+  double free4_omax = 0.0;
   uint64_t free_big_mask = ~0ull;   // oversized leaves the search-tree walk still tests from its list
   DNode* d_free = nullptr;
   DShadowProof occ{};               // build_occluders (the root box's face triangles)
@@ -237,6 +240,8 @@ static void free_scene_dev(rrt_ctx* c) {
   hipFree(c->d_big_mask);
   hipFree(c->d_free);
   c->d_free = nullptr;
+  hipFree(c->d_free4);
+  c->d_free4 = nullptr;
   c->d_grid = nullptr; c->d_clean = nullptr; c->d_big = nullptr; c->d_planes = nullptr; c->d_big_mask = nullptr;
   c->d_nodes = nullptr; c->d_geo = nullptr; c->d_nrm = nullptr; c->d_meta = nullptr; c->d_bsdfs = nullptr;
   c->d_lights = nullptr;
@@ -879,6 +884,69 @@ static void build_free_tree(rrt_ctx* c) {
   for (size_t i = 0; i < out.size(); ++i) out[i].skip = end[i] < (int32_t)out.size() ? end[i] : -1;
 }
 
+// The search tree 4 wide: each node holds the boxes of a binary inner node's children, the inner
+// ones opened (largest surface first) until there are four -- the search tree's nodes two levels
+// down.  A walk then tests four boxes per dependent load instead of one (the slow pixels' walks
+// are chains of ~40 dependent box tests per micro segment: tools/ notes in DESIGN.md §5).  Node
+// indices fit 16 bits (the walk's register stack); larger trees keep the binary walk.
+static void build_free4(rrt_ctx* c) {
+  c->free4.clear();
+  const std::vector<DNode>& t = c->free_tree;
+  if (t.size() < 3 || t[0].count != 0) return;
+  // f32 boxes: rounded outward, then widened by pad = 1e-4 of the scene's coordinate scale -- far
+  // above the f32 pre-test's rounding for segment origins within free4_omax = 8 x that scale
+  // (origin error <= 2^-24 x 8 scale, quotient error <= 2^-22 relative: both < 1e-6 of the scale)
+  double sc = 1.0;
+  for (int k = 0; k < 3; ++k) sc = std::max(sc, std::max(std::fabs(t[0].mn[k]), std::fabs(t[0].mx[k])));
+  if (!std::isfinite(sc)) return;
+  const double pad = 1e-4 * sc;
+  c->free4_omax = 8.0 * sc;
+  auto down = [&](double v) { float f = (float)(v - pad); while ((double)f > v - pad) f = std::nextafter(f, -INFINITY); return f; };
+  auto up = [&](double v) { float f = (float)(v + pad); while ((double)f < v + pad) f = std::nextafter(f, INFINITY); return f; };
+  auto area = [&](int32_t i) {
+    const double ex = t[i].mx[0] - t[i].mn[0], ey = t[i].mx[1] - t[i].mn[1], ez = t[i].mx[2] - t[i].mn[2];
+    return ex * ey + ey * ez + ez * ex;
+  };
+  // children of binary inner node b (pre-order: left = b + 1, right = the left subtree's successor)
+  auto kids = [&](int32_t b, int32_t& l, int32_t& r) { l = b + 1; r = t[l].skip; };
+  std::function<int32_t(int32_t)> rec = [&](int32_t b) -> int32_t {
+    const int32_t me = (int32_t)c->free4.size();
+    c->free4.push_back(DNode4{});
+    int32_t ch[4], n = 0;
+    kids(b, ch[0], ch[1]);
+    n = 2;
+    while (n < 4) {  // open the largest inner child
+      int best = -1;
+      for (int i = 0; i < n; ++i)
+        if (t[ch[i]].count == 0 && (best < 0 || area(ch[i]) > area(ch[best]))) best = i;
+      if (best < 0) break;
+      int32_t l, r;
+      kids(ch[best], l, r);
+      ch[best] = l;
+      ch[n++] = r;
+    }
+    int32_t sub[4];
+    for (int i = 0; i < n; ++i) sub[i] = t[ch[i]].count == 0 ? rec(ch[i]) : -1;
+    DNode4& d = c->free4[me];
+    for (int i = 0; i < 4; ++i) {
+      if (i >= n) {
+        d.mnx[i] = d.mny[i] = d.mnz[i] = INFINITY;
+        d.mxx[i] = d.mxy[i] = d.mxz[i] = -INFINITY;
+        d.child[i] = -1; d.first[i] = 0; d.count[i] = -1;
+        continue;
+      }
+      const DNode& s = t[ch[i]];
+      d.mnx[i] = down(s.mn[0]); d.mny[i] = down(s.mn[1]); d.mnz[i] = down(s.mn[2]);
+      d.mxx[i] = up(s.mx[0]); d.mxy[i] = up(s.mx[1]); d.mxz[i] = up(s.mx[2]);
+      d.child[i] = s.count == 0 ? sub[i] : ch[i];
+      d.first[i] = s.first; d.count[i] = s.count;
+    }
+    return me;
+  };
+  rec(0);
+  if (c->free4.size() > 65535) c->free4.clear();
+}
+
 static int upload(rrt_ctx* c, void** dst, const void* src, size_t bytes) {
   if (bytes == 0) bytes = 16;
   HIPCHK(c, hipMalloc(dst, bytes));
@@ -1045,6 +1113,7 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   build_occluders(c);
   build_clean_tree(c, c->clean, c->big);
   build_free_tree(c);
+  build_free4(c);
   build_big_masks(c);
   {  // plane-cull margin: 1e-9 of the scene's coordinate scale (rounding is ~1e-16 of it)
     const Box& rb = c->nodes[0].bb;
@@ -1076,6 +1145,9 @@ extern "C" int rrt_set_scene(rrt_ctx* c, const rrt_scene_desc* s) {
   if ((rc = upload(c, (void**)&c->d_planes, planes.data(), planes.size() * sizeof(DPlane)))) return rc;
   if (!c->free_tree.empty() &&
       (rc = upload(c, (void**)&c->d_free, c->free_tree.data(), c->free_tree.size() * sizeof(DNode))))
+    return rc;
+  if (!c->free4.empty() &&
+      (rc = upload(c, (void**)&c->d_free4, c->free4.data(), c->free4.size() * sizeof(DNode4))))
     return rc;
   if (c->has_clean) {
     if ((rc = upload(c, (void**)&c->d_clean, c->clean.data(), c->clean.size() * sizeof(DNode)))) return rc;
@@ -1322,6 +1394,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     } else {
       kp.free_nodes = c->d_free;  // over the clean tree's leaves (+ kp.big), or every leaf
       kp.free_big_mask = c->free_big_mask;
+      // the 4-wide walk of the same tree (A/B: RRT_AB_NO_BVH4=1 in the environment)
+      const char* nb4 = std::getenv("RRT_AB_NO_BVH4");
+      kp.free4 = (nb4 && nb4[0] == '1') ? nullptr : c->d_free4;
+      kp.free4_omax = c->free4_omax;
     }
   }
   kp.planes = c->d_planes; kp.plane_eps = c->plane_eps;
@@ -2099,6 +2175,21 @@ extern "C" int rrt_get_search_tree(const rrt_ctx* c, double* boxes, int32_t* nod
     if (nodes) { nodes[4 * i] = n.skip; nodes[4 * i + 1] = n.first; nodes[4 * i + 2] = n.count; nodes[4 * i + 3] = n.pad; }
   }
   return (int)c->free_tree.size();
+}
+
+extern "C" int rrt_get_search_tree4(const rrt_ctx* c, float* boxes, int32_t* kids) {
+  if (!c || !c->has_scene) return RRT_E_INVALID;
+  for (size_t i = 0; i < c->free4.size(); ++i) {
+    const DNode4& n = c->free4[i];
+    for (int j = 0; j < 4; ++j) {
+      if (boxes) {
+        float* b = boxes + 24 * i + 6 * j;
+        b[0] = n.mnx[j]; b[1] = n.mny[j]; b[2] = n.mnz[j]; b[3] = n.mxx[j]; b[4] = n.mxy[j]; b[5] = n.mxz[j];
+      }
+      if (kids) { kids[12 * i + 3 * j] = n.child[j]; kids[12 * i + 3 * j + 1] = n.first[j]; kids[12 * i + 3 * j + 2] = n.count[j]; }
+    }
+  }
+  return (int)c->free4.size();
 }
 
 extern "C" int rrt_get_clean_tree(const rrt_ctx* c, double* boxes, int32_t* nodes, double* big_boxes,

@@ -24,6 +24,18 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 64, "DNode must be 64 bytes");
 
+// 4-wide node of the search tree (rrt_host.cpp build_free4; rrt_device.h traverse_free4): the boxes of
+// up to four children -- the search tree's nodes two levels down -- as structure of arrays, in f32
+// rounded outward and widened by KParams::free4_pad: a conservative pre-test only (a leaf child that
+// passes it takes the exact test on its own f64 box, kp.free_nodes[child]).  A child is an inner node
+// (count 0: child = DNode4 index), a leaf of the search tree (count > 0: slots [first, first + count),
+// child = its search-tree node index, the replay's ref) or empty (count < 0).
+struct alignas(16) DNode4 {
+  float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
+  int32_t child[4], first[4], count[4], pad[4];
+};
+static_assert(sizeof(DNode4) == 160, "DNode4 must be 160 bytes");
+
 // Oversized leaf of the reference tree, tested directly by the clean-tree walk
 // (rrt_device.h traverse_clean): its box, leaf slots and left-first leaf ordinal.
 struct alignas(16) DBig {
@@ -196,6 +208,8 @@ struct KParams {
   int32_t clean_root;         // 0, or -1 if every leaf is oversized
   uint32_t n_big;
   const DNode* free_nodes;    // search tree over the clean tree's leaves (traverse_free), or null
+  const DNode4* free4;        // the same tree 4 wide (traverse_free4), or null (binary walk)
+  double free4_omax;          // segments starting farther out (max |coordinate|) take the binary walk
   DCamera cam;
   DHole hole;
   DMissProof miss;

@@ -1180,6 +1180,15 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   const uint64_t t_end = clock64(), w_end = wall_clock64();
   uint64_t v[12] = {t_end - t_start, cn.t_query, cn.t_micro, cn.t_trav, cn.t_proof, cn.t_squery, cn.t_strav, 0,
                     cn.t_claim, cn.t_chain, cn.t_shade, cn.t_fold};
+  {  // lane sums of the phases (slot 12 + i): a phase's lane use = lane sum / (64 x busiest lane)
+    const int ks[8] = {0, 1, 2, 3, 4, 5, 6, 10};
+    const int slot[8] = {15, 12, 23, 21, 14, 13, 22, 20};
+    for (int i = 0; i < 8; ++i) {
+      uint64_t sm = v[ks[i]];
+      for (int off2 = 32; off2 > 0; off2 >>= 1) sm += __shfl_xor(sm, off2);
+      if (lane == 0) atomicAdd(&rrt_prof[slot[i]], (unsigned long long)sm);
+    }
+  }
   for (int k = 0; k < 12; ++k) {
     for (int off2 = 32; off2 > 0; off2 >>= 1) {
       const uint64_t o2 = __shfl_xor(v[k], off2);

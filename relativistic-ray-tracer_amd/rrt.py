@@ -108,7 +108,7 @@ EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rr
            "rrt_camera_state_desc", "rrt_set_envmap", "rrt_tonemap_pixel", "rrt_write_png",
            "rrt_exr_load", "rrt_exr_free", "rrt_exr_save", "rrt_kerr_frame", "rrt_get_big_masks",
            "rrt_get_occluders", "rrt_group_create", "rrt_group_render", "rrt_group_destroy", "rrt_libm_eval",
-           "rrt_set_proof_audit", "rrt_get_proof_audit"]
+           "rrt_set_proof_audit", "rrt_get_proof_audit", "rrt_get_search_tree4"]
 AUDIT_KINDS = ("camera", "shadow", "pixel", "strip", "kerr", "zero")  # include/rrt.h RRT_AUDIT_*
 
 _lib = None
@@ -162,6 +162,7 @@ def lib():
         L.rrt_proof_envelope.argtypes = [vp]
         L.rrt_get_bvh.argtypes = [vp, vp, vp, vp]
         for name, n_args in (("rrt_get_free_grid", 4), ("rrt_get_clean_tree", 5), ("rrt_get_search_tree", 3),
+                             ("rrt_get_search_tree4", 3),
                              ("rrt_get_big_masks", 3),
                              ("rrt_get_occluders", 3)):
             if hasattr(L, name):  # absent from older builds loaded through RRT_LIB
@@ -447,6 +448,16 @@ class Renderer:
         if k < 0:
             self._chk(k)
         return tot[:k], main[:k]
+
+    def search_tree4(self):
+        """(boxes [n, 4, 6] f32, kids [n, 4, 3] = child, first, count) of the 4-wide walk's nodes."""
+        n = lib().rrt_get_search_tree4(self.h, None, None)
+        if n < 0:
+            self._chk(n)
+        b = np.zeros((max(n, 1), 4, 6), np.float32)
+        k = np.zeros((max(n, 1), 4, 3), np.int32)
+        lib().rrt_get_search_tree4(self.h, _p(b), _p(k))
+        return b[:n], k[:n]
 
     def free_grid(self):
         """(k [nz][ny][nx] uint8, g0 (3,), inv_h, h_free) of the empty-space grid, or None."""

@@ -21,14 +21,17 @@ import numpy as np
 from miss_proof_sim import ETA, KAPPA, _step0, seg_clear
 
 
-def nocc_box(T, faces):
-    """rrt_host.cpp build_occluders' box of every triangle but the kept ones (spheres: none in the
-    scenes these mirror-tests use)."""
+def nocc_box(T, faces, spheres=()):
+    """rrt_host.cpp build_occluders' box of every primitive but the kept face triangles: the other
+    triangles of T and the spheres [(centre, radius)]."""
     kept = {t[4] for f in faces for t in f}
     rest = np.array([i for i in range(len(T)) if i not in kept], np.int64)
-    if len(rest) == 0:
+    pts = [T[rest].reshape(-1, 3)] if len(rest) else []
+    for cen, rad in spheres:
+        pts.append(np.array([np.asarray(cen) - rad, np.asarray(cen) + rad]))
+    if not pts:
         return np.full(3, np.inf), np.full(3, -np.inf)
-    P = T[rest].reshape(-1, 3)
+    P = np.concatenate(pts)
     return P.min(0), P.max(0)
 
 

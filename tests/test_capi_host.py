@@ -17,7 +17,7 @@ SCENES = sorted(f[:-5] for f in os.listdir(os.path.join(GOLD, "scenes")) if f.en
 
 def test_exports_match_header():
     hdr = open(os.path.join(ROOT, "include", "rrt.h")).read()
-    declared = set(re.findall(r"\b(rrt_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(rrt_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(rrt.EXPORTS), declared ^ set(rrt.EXPORTS)
     L = rrt.lib()
     for name in declared:
@@ -424,3 +424,55 @@ def test_group_rejects_host_contexts():
     assert L.rrt_group_create(arr, 2, C.byref(g)) == rrt.RRT_E_NO_DEVICE
     assert L.rrt_group_create(None, 0, C.byref(g)) == rrt.RRT_E_INVALID
     L.rrt_destroy(h)
+
+
+@pytest.mark.parametrize("scene", ["CBbunny", "CBspheres_lambertian", "CBcoil", "CBgems"])
+def test_search_tree4_covers_the_search_tree(host_ctx, scene):
+    """The 4-wide walk's nodes (rrt_host.cpp build_free4): every search-tree leaf below the root is a
+    leaf child of exactly one node, with its slot run; every inner child is a node reached once; each
+    child's f32 box contains the f64 boxes of every search-tree node below it (a conservative
+    pre-test: it never fails a box the exact test passes)."""
+    sf = rrt.SceneFile(os.path.join(GOLD, "scenes", scene + ".rrts"))
+    host_ctx.set_scene(sf)
+    sboxes, snodes = host_ctx.search_tree()
+    b4, k4 = host_ctx.search_tree4()
+    if len(snodes) < 3:
+        assert len(b4) == 0
+        return
+    assert 0 < len(b4) <= 65535
+    leaves = [i for i in range(len(snodes)) if snodes[i, 2] != 0]
+    seen, reached = [], [0]
+
+    def below(i):  # search-tree nodes of i's subtree (pre-order: i .. skip(i) - 1)
+        end = snodes[i, 0] if snodes[i, 0] >= 0 else len(snodes)
+        return range(i, end)
+
+    def node_box_cover(n4, j, subtree_root):
+        b = b4[n4, j].astype(np.float64)
+        for s in below(subtree_root):
+            assert np.all(b[:3] <= sboxes[s, :3]) and np.all(b[3:] >= sboxes[s, 3:]), (n4, j, s)
+
+    # map each 4-wide child back to a search-tree subtree: leaves by index, inner nodes by the union
+    # of the leaves they reach
+    def walk(n4):
+        leaf_set = []
+        for j in range(4):
+            child, first, count = k4[n4, j]
+            if count < 0:
+                continue
+            if count > 0:
+                assert snodes[child, 2] == count and snodes[child, 1] == first
+                seen.append(int(child))
+                node_box_cover(n4, j, child)
+                leaf_set.append(int(child))
+            else:
+                reached.append(int(child))
+                sub = walk(child)
+                for s in sub:
+                    bb = b4[n4, j].astype(np.float64)
+                    assert np.all(bb[:3] <= sboxes[s, :3]) and np.all(bb[3:] >= sboxes[s, 3:])
+                leaf_set += sub
+        return leaf_set
+    walk(0)
+    assert sorted(seen) == leaves
+    assert sorted(reached) == list(range(len(b4)))

@@ -33,17 +33,19 @@ def scene_tables(sf):
     """per-triangle bsdf type (SceneFile.triangles() order) and the area lights' vectors"""
     d = rrt.SceneDesc.from_address(sf.desc())
     btype = [C.cast(d.bsdfs, C.POINTER(C.c_uint32))[15 * i] for i in range(d.n_bsdfs)]
-    tb = []
+    tb, spheres = [], []
     for i in range(d.n_objects):
         o = d.objects[i]
         if o.kind == 0:
             tb += [btype[o.bsdf]] * o.n_triangles
+        else:
+            spheres.append((np.array(o.center[:]), float(o.radius)))
     lights = []
     for i in range(d.n_lights):
         L = d.lights[i]
         if L.type == 0:
             lights.append((np.array(L.radiance[:], np.float32), np.array([[L.v[k][j] for j in range(3)] for k in range(4)])))
-    return np.array(tb), lights
+    return np.array(tb), lights, spheres
 
 
 def main():
@@ -57,7 +59,7 @@ def main():
     c = Case(a.case)
     sf = rrt.SceneFile(c.scene_path)
     T = sf.triangles()
-    tb, lights = scene_tables(sf)
+    tb, lights, spheres = scene_tables(sf)
     r = rrt.Renderer(device=-1)
     r.set_scene(sf)
     boxes, _, _ = r.bvh()
@@ -65,7 +67,7 @@ def main():
     lo, hi = boxes[0][:3].copy(), boxes[0][3:].copy()
     faces, w = occluders(T, lo, hi)
     emit = [sum(1 << i for i, t in enumerate(faces[f]) if tb[t[4]] == 1) for f in range(6)]
-    nlo, nhi = nocc_box(T, faces)
+    nlo, nhi = nocc_box(T, faces, spheres)
     osc = O.Scene(c.scene_path)
     cam = O.load_camera(c.camera_path)
     cols = np.array(cam.c2w, np.float64).reshape(3, 3).T.ravel().copy()

@@ -119,6 +119,11 @@ def main():
                    "outside_queries_and_proof": 1 - (tq + tp + tsq) / tot,
                    "claim": float(buf[16]) / tot, "chain": float(buf[17]) / tot, "shade_incl_shadow": float(buf[18]) / tot,
                    "fold": float(buf[19]) / tot,
+                   # lanes active in each phase (lane sum / (64 x busiest lane), summed over waves)
+                   "lane_use": {k: float(buf[i]) / (64.0 * float(buf[j])) if buf[j] else None for k, i, j in
+                                (("total", 15, 0), ("camera_query", 12, 1), ("micro", 23, 2), ("camera_walk", 21, 3),
+                                 ("miss_proof", 14, 4), ("shadow_query", 13, 5), ("shadow_walk", 22, 6),
+                                 ("shade", 20, 18))},
                    "slowest_pixels": slow_px,
                    "busy_frac_working_waves": float(((ends - starts)[res]).sum() / max(res.sum(), 1)),
                    "working_wave_end_q": [round(float(q), 3) for q in np.quantile(ends[res], [0.05, 0.25, 0.5, 0.75, 0.95, 1.0])],
