@@ -41,8 +41,9 @@ def _params(c, flags):
 # fields of view see only the room, so there the shadow proof is what runs)
 AUDIT_CASES = [("cfg3_bunny_1080p_s64", (832, 412, 256, 256), False), ("cfg3_bunny_1080p_s64", (0, 0, 192, 192), True),
                ("cfg2_spheres_1080p_s64_flat", (1600, 800, 128, 128), True), ("bunny_160x120_s16", None, False),
-               ("bunny_B1_160x120_s16", None, False), ("spheres_B2_160x120_s16", None, False),
-               ("cfg4_knot_240x135_s16", None, False), ("empty_64x48_s8", None, False)]
+               ("bunny_B1_160x120_s16", None, False), ("spheres_B2_160x120_s16", None, False)]
+# (the point-light scenes -- cfg4's knot -- and the empty room carry no occluder for the shadow
+# proof, and their small frames see no misses: nothing to audit there)
 
 
 @pytest.mark.parametrize("name,region,misses", AUDIT_CASES)
