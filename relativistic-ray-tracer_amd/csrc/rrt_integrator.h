@@ -64,13 +64,76 @@ __device__ __forceinline__ spec one_bounce(const KParams& kp, Rng& g, const Isec
                               : direct_importance<COUNT, general_of(LEAN), DEEP>(kp, g, is, cn);
 }
 
+// The per-level terms of at_least_one_bounce (the recursion's pending values): the level's direct
+// light Ld, its flags (child: the bounce ray hit, so the level folds the child's radiance in; dl: the
+// BSDF is a delta), and for a child the BSDF sample, |cos|, pdf and the hit's emission.
+// LevelsPriv: private arrays, any depth <= RRT_MAX_DEPTH (they live in scratch: dynamic indices).
+struct LevelsPriv {
+  static constexpr int D = RRT_MAX_DEPTH;
+  spec Ld[D], smp[D], cem[D];
+  float cs[D], pd[D];
+  bool child[D], dl[D];
+  __device__ __forceinline__ void level(int k, spec ld, bool d) { Ld[k] = ld; child[k] = false; dl[k] = d; }
+  __device__ __forceinline__ void bounce(int k, spec sm, float c, float p, spec em) {
+    child[k] = true; smp[k] = sm; cs[k] = c; pd[k] = p; cem[k] = em;
+  }
+  __device__ __forceinline__ spec fold(int k) const {
+    spec L = S(0, 0, 0);
+    for (int j = k; j >= 0; --j) {
+      spec Lj = Ld[j];
+      if (child[j]) {
+        spec Lc = L;
+        if (dl[j]) Lc = Lc + cem[j];
+        Lj = Lj + (((Lc * smp[j]) * cs[j]) / pd[j]) / (float)0.7;
+      }
+      L = Lj;
+    }
+    return L;
+  }
+};
+// LevelsLds: the same terms in LDS, one column per thread of a 256-thread block, for frames of
+// max_ray_depth <= D (the loop then never reaches RRT_MAX_DEPTH's cap): the bounce kernel's levels
+// left scratch, whose writes were most of its HBM traffic (bounce paths).
+template <int D_>
+struct LevelLds {
+  float v[11][D_][256];  // Ld rgb, smp rgb, cem rgb, cs, pd
+  uint8_t fl[D_][256];   // 1: child, 2: dl
+};
+template <int D_>
+struct LevelsLds {
+  static constexpr int D = D_;
+  LevelLds<D_>* p;
+  uint32_t t;
+  __device__ __forceinline__ void level(int k, spec ld, bool d) {
+    p->v[0][k][t] = ld.r; p->v[1][k][t] = ld.g; p->v[2][k][t] = ld.b;
+    p->fl[k][t] = d ? 2 : 0;
+  }
+  __device__ __forceinline__ void bounce(int k, spec sm, float c, float pp, spec em) {
+    p->v[3][k][t] = sm.r; p->v[4][k][t] = sm.g; p->v[5][k][t] = sm.b;
+    p->v[6][k][t] = em.r; p->v[7][k][t] = em.g; p->v[8][k][t] = em.b;
+    p->v[9][k][t] = c; p->v[10][k][t] = pp;
+    p->fl[k][t] |= 1;
+  }
+  __device__ __forceinline__ spec fold(int k) const {
+    spec L = S(0, 0, 0);
+    for (int j = k; j >= 0; --j) {
+      spec Lj = S(p->v[0][j][t], p->v[1][j][t], p->v[2][j][t]);
+      const uint8_t f = p->fl[j][t];
+      if (f & 1) {
+        spec Lc = L;
+        if (f & 2) Lc = Lc + S(p->v[6][j][t], p->v[7][j][t], p->v[8][j][t]);
+        Lj = Lj + (((Lc * S(p->v[3][j][t], p->v[4][j][t], p->v[5][j][t])) * p->v[9][j][t]) / p->v[10][j][t]) / (float)0.7;
+      }
+      L = Lj;
+    }
+    return L;
+  }
+};
+
 // at_least_one_bounce_radiance (:69-101) unrolled into a loop: the recursion is walked down
 // storing each level's terms, then folded back up in the reference's evaluation order.
-template <bool COUNT, int LEAN>
-__device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn) {
-  spec Ld[RRT_MAX_DEPTH], smp[RRT_MAX_DEPTH], cem[RRT_MAX_DEPTH];
-  float cs[RRT_MAX_DEPTH], pd[RRT_MAX_DEPTH];
-  bool child[RRT_MAX_DEPTH], dl[RRT_MAX_DEPTH];
+template <bool COUNT, int LEAN, class LV = LevelsPriv>
+__device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, Isect cur, Counters& cn, LV lv = LV()) {
   uint32_t depth = kp.max_ray_depth;
   int k = 0;
   for (;; ++k) {
@@ -80,19 +143,15 @@ __device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, I
     spec L_out = S(0, 0, 0);
     if (!is_delta(b)) L_out = L_out + one_bounce<COUNT, general_of(LEAN), true>(kp, g, cur, cn);
     if (LEAN == V_SW && sw_illum(kp) == 3u && depth == kp.max_ray_depth) L_out = S(0, 0, 0);  // ILLUM 3 (:78-81)
-    Ld[k] = L_out;
-    child[k] = false;
-    dl[k] = is_delta(b);
+    lv.level(k, L_out, is_delta(b));
     if (depth == kp.max_ray_depth || (depth > 1 && g.coin(0.7))) {
       v3 w_in; float pdf;
       spec sample = bsdf_sample_f(b, g, w_out, w_in, pdf, LEAN == V_SW && (kp.sw & SW_MF_HEMI));
       if (pdf == 0.0f) break;
       v3 wi_world = to_world(f, w_in);
       Isect is2;
-      if (trace<false, COUNT, true, LEAN>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < RRT_MAX_DEPTH) {
-        child[k] = true;
-        smp[k] = sample; cs[k] = (float)fabs(w_in.z); pd[k] = pdf;
-        cem[k] = emission(kp.bsdfs[is2.bsdf]);
+      if (trace<false, COUNT, true, LEAN>(kp, cur.hit_p + smul(EPS_D, wi_world), wi_world, &is2, cn) && k + 1 < LV::D) {
+        lv.bounce(k, sample, (float)fabs(w_in.z), pdf, emission(kp.bsdfs[is2.bsdf]));
         cur = is2;
         depth -= 1;
         continue;
@@ -100,17 +159,7 @@ __device__ __forceinline__ spec at_least_one_bounce(const KParams& kp, Rng& g, I
     }
     break;
   }
-  spec L = S(0, 0, 0);
-  for (int j = k; j >= 0; --j) {
-    spec Lj = Ld[j];
-    if (child[j]) {
-      spec Lc = L;
-      if (dl[j]) Lc = Lc + cem[j];
-      Lj = Lj + (((Lc * smp[j]) * cs[j]) / pd[j]) / (float)0.7;
-    }
-    L = Lj;
-  }
-  return L;
+  return lv.fold(k);
 }
 
 }  // namespace rrt

@@ -9,10 +9,13 @@
 // sample-parallel batch kernel of rrt_sample.hip instead.
 #include "rrt_integrator.h"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace rrt {
 
-template <bool DEEP, bool COUNT, int LEAN, int W = 0>
-__device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn) {  // :103-123
+template <bool DEEP, bool COUNT, int LEAN, int W = 0, class LV = LevelsPriv>
+__device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3 d, Counters& cn, LV lv = LV()) {  // :103-123
   Isect is;
   if (camera_proven_miss<COUNT, LEAN == V_KERR, LEAN == 0, W>(kp, o, d, cn) ||
       !trace<false, COUNT, DEEP, LEAN>(kp, o, d, &is, cn))  // miss: envLight->sample_dir(r), unbent r
@@ -22,17 +25,18 @@ __device__ __forceinline__ spec est_radiance(const KParams& kp, Rng& g, v3 o, v3
     if (il == 0u)  // normal_shading (pathtracer.h:199-201): Spectrum(n) * .5 + Spectrum(.5, .5, .5)
       return S((float)is.n.x, (float)is.n.y, (float)is.n.z) * (float).5 + S(.5f, .5f, .5f);
     if (il == 1u) return one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
-    return at_least_one_bounce<COUNT, LEAN>(kp, g, is, cn);
+    return at_least_one_bounce<COUNT, LEAN>(kp, g, is, cn, lv);
   }
   spec e = emission(kp.bsdfs[is.bsdf]);
   if (kp.max_ray_depth == 0) return e;
   if (!DEEP || kp.max_ray_depth == 1) return e + one_bounce<COUNT, LEAN, DEEP>(kp, g, is, cn);
-  return e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
+  return e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn, lv);
 }
 
 // PathTracer::raytrace_pixel (:125-163): ADAPTIVE 1, THIN_LENS 0 -- or, in the V_SW build, as kp.sw says
-template <bool DEEP, bool COUNT, int LEAN, int W = 0>
-__device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn) {
+template <bool DEEP, bool COUNT, int LEAN, int W = 0, class LV = LevelsPriv>
+__device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, uint32_t y, int& count, Rng& g, Counters& cn,
+                                               LV lv = LV()) {
   spec ret = S(0, 0, 0);
   int n = 0;  // samples taken (the reference's i after its loop; counted explicitly: the
               // `++i; break;` form was miscompiled in the register-starved bounce build)
@@ -55,11 +59,11 @@ __device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, ui
       const v3 c0 = ld3(cam.c2w0), c1 = ld3(cam.c2w1), c2 = ld3(cam.c2w2);
       const v3 o = ld3(cam.pos) + ((smul(pl.x, c0) + smul(pl.y, c1)) + smul(pl.z, c2));  // pos + c2w * pLens
       const v3 q = V(vx * kp.focal, vy * kp.focal, -1.0 * kp.focal) - pl;                // pinHole * f - pLens
-      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, o, unit((smul(q.x, c0) + smul(q.y, c1)) + smul(q.z, c2)), cn);
+      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, o, unit((smul(q.x, c0) + smul(q.y, c1)) + smul(q.z, c2)), cn, lv);
     } else {
       // Camera::generate_ray (part1_code.cpp:182-187)
       v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
-      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, ld3(cam.pos), unit(w), cn);
+      s = est_radiance<DEEP, COUNT, LEAN, W>(kp, g, ld3(cam.pos), unit(w), cn, lv);
     }
     ret = ret + s;
     if (LEAN == V_SW && (kp.sw & SW_NO_ADAPTIVE)) { n = i + 1; continue; }  // ADAPTIVE 0
@@ -81,11 +85,13 @@ __device__ __forceinline__ spec raytrace_pixel(const KParams& kp, uint32_t x, ui
 // ------------------------------------------------------------------ kernels
 // DEEP: max_ray_depth >= 2 (bounce loop); COUNT: per-pixel work counters; LEAN: area lights
 // only, no microfacet BSDF, importance-sampled direct light (the BASELINE scenes); WAVES: the
-// register budget, as minimum waves per SIMD.
-template <bool DEEP, bool COUNT, int LEAN, int WAVES>
+// register budget, as minimum waves per SIMD; LVD: 0, or the depth bound of the bounce levels kept
+// in LDS (rrt_integrator.h LevelsLds; frames of max_ray_depth <= LVD).
+template <bool DEEP, bool COUNT, int LEAN, int WAVES, int LVD = 0>
 __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* __restrict__ kpp) {
   const KParams& kp = *kpp;
   using namespace rrt;
+  using LV = std::conditional_t<(LVD > 0), LevelsLds<(LVD > 0 ? LVD : 1)>, LevelsPriv>;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t bpt = kp.blocks_per_tile_side;
   const uint32_t tpix = kp.tile_size * kp.tile_size;
@@ -117,7 +123,12 @@ __global__ __launch_bounds__(256, WAVES) void rrt_render_kernel(const KParams* _
       Rng g; g.key = rrt_pixel_key(kp.seed, x, y); g.ctr = 0;
       Counters cn = {0, 0, 0, 0};
       int cnt;
-      spec s = raytrace_pixel<DEEP, COUNT, LEAN, 16 * DEEP + 8 * COUNT + WAVES>(kp, x, y, cnt, g, cn);
+      LV lv;
+      if constexpr (LVD > 0) {
+        __shared__ LevelLds<(LVD > 0 ? LVD : 1)> lvs;
+        lv = LV{&lvs, threadIdx.x};
+      }
+      spec s = raytrace_pixel<DEEP, COUNT, LEAN, 16 * DEEP + 8 * COUNT + WAVES>(kp, x, y, cnt, g, cn, lv);
       const size_t k = (size_t)t * tpix + (size_t)ly * kp.tile_size + lx;
       kp.rgb[3 * k] = s.r; kp.rgb[3 * k + 1] = s.g; kp.rgb[3 * k + 2] = s.b;
       kp.count[k] = cnt;
@@ -188,6 +199,9 @@ __global__ void rrt_libm_kernel(int fn, uint64_t n, const double* a, const doubl
 hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, int count, int lean, int waves, uint32_t grid,
                              hipStream_t stream) {
 #define RRT_LAUNCH(D, C, L, W) hipLaunchKernelGGL((rrt_render_kernel<D, C, L, W>), dim3(grid), dim3(256), 0, stream, d_kp)
+  // the bounce levels in LDS (frames of max_ray_depth <= 4; RRT_AB_NO_LEVEL_LDS=1 keeps them private, A/B)
+  static const bool no_lv = [] { const char* e = std::getenv("RRT_AB_NO_LEVEL_LDS"); return e && e[0] == '1'; }();
+  const bool lv4 = deep && !count && kp.max_ray_depth <= 4u && !no_lv;
   if (lean == rrt::V_SW) {  // the reference's switches as run-time flags: one bounce-capable build
     if (count) RRT_LAUNCH(true, true, rrt::V_SW, 1); else RRT_LAUNCH(true, false, rrt::V_SW, 1);
   } else if (lean == rrt::V_KERR) {  // the Kerr builds (general integrator)
@@ -202,6 +216,10 @@ hipError_t rrt_launch_render(const KParams& kp, const KParams* d_kp, int deep, i
     if (count) {
       RRT_LAUNCH(true, true, false, 1);
     } else {
+      if (lv4 && (waves == 3 || waves <= 0 || waves > 4)) {
+        hipLaunchKernelGGL((rrt_render_kernel<true, false, false, 3, 4>), dim3(grid), dim3(256), 0, stream, d_kp);
+        return hipGetLastError();
+      }
       switch (waves) {  // register budget (A/B): the bounce build spills below 1 wave/SIMD's 256 VGPRs
         case 2: RRT_LAUNCH(true, false, false, 2); break;
         case 3: RRT_LAUNCH(true, false, false, 3); break;

@@ -319,6 +319,12 @@ extern "C" int rrt_prof_read_slow(unsigned long long* out) {  // out: 64; resets
 }
 // per pixel slot (slot < 2^21, e.g. 1080p): elapsed wall ticks (claim to stop, 24 bits) << 8 | rounds
 __device__ uint32_t rrt_prof_px[1u << 21];
+// per pixel slot: the wall clock (low 32 bits) when the pixel stopped
+__device__ uint32_t rrt_prof_px_end[1u << 21];
+extern "C" int rrt_prof_read_px_end(uint32_t* out, uint32_t n) {  // reads min(n, 2^21) slots
+  n = n < (1u << 21) ? n : (1u << 21);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof_px_end), n * sizeof(uint32_t)) == hipSuccess ? 0 : -1;
+}
 extern "C" int rrt_prof_read_px(uint32_t* out, uint32_t n) {  // reads and resets min(n, 2^21) slots
   n = n < (1u << 21) ? n : (1u << 21);
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rrt_prof_px), n * sizeof(uint32_t)) != hipSuccess) return -1;
@@ -725,7 +731,10 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
     if (t == 0) {
       const uint32_t ts = kp.tile_size, tpix = ts * ts;
       const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + claim_r(ix % tpix, ts);
-      if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
+      if (slot < (1u << 21)) {
+        rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
+        rrt_prof_px_end[slot] = (uint32_t)wall_clock64();
+      }
     }
 #endif
   }
@@ -1156,7 +1165,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
           atomicMax(&rrt_prof_slow[slot & 63u], (el << 38) | ((unsigned long long)min(px_rounds, 127u) << 31) |
                                                     ((unsigned long long)min(px_steps, 127u) << 24) |
                                                     (unsigned long long)(slot & 0xffffffu));
-          if (slot < (1u << 21)) rrt_prof_px[slot] = ((uint32_t)min(el, (uint64_t)0xffffff) << 8) | min(px_rounds, 255u);
+          if (slot < (1u << 21)) {
+            rrt_prof_px[slot] = ((uint32_t)min(el, (uint64_t)0xffffff) << 8) | min(px_rounds, 255u);
+            rrt_prof_px_end[slot] = (uint32_t)wall_clock64();
+          }
         }
 #endif
         const spec r = ret / (float)i;

@@ -103,7 +103,15 @@ def main():
             ok = (xs < frame_w) & (ys < frame_h)
             img_t[ys[ok], xs[ok]] = (pxv[ok] >> 8) / (span / ms)
             img_r[ys[ok], xs[ok]] = pxv[ok] & 255
-            np.savez_compressed(f"gpurun_out/px_{a.case}_{fl}.npz", ms=img_t, rounds=img_r)
+            # when each pixel stopped, as a fraction of the kernel's span (-1: not rendered here)
+            L.rrt_prof_read_px_end.argtypes = [C.c_void_p, C.c_uint32]
+            pxe = np.zeros(n, np.uint32)
+            L.rrt_prof_read_px_end(pxe.ctypes.data, n)
+            img_e = np.full((frame_h, frame_w), -1.0, np.float32)
+            rel = ((pxe.astype(np.int64) - (t0 & 0xffffffff)) % (1 << 32)) / span
+            got = ok & (pxv > 0)
+            img_e[ys[got], xs[got]] = rel[got]
+            np.savez_compressed(f"gpurun_out/px_{a.case}_{fl}.npz", ms=img_t, rounds=img_r, end=img_e)
         slow = np.zeros(64, np.uint64)
         L.rrt_prof_read_slow(slow.ctypes.data)
         slow_px = []
