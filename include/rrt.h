@@ -326,8 +326,10 @@ int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 /* Diagnostics: evaluate the device's restatement of the host C library's transcendentals
  * (csrc/rrt_glibm.h -- the reference's sin/cos (sampler.cpp:53-55, environment_light.cpp:97-137),
  * acos (sampler.cpp:20, bsdf.h:166, environment_light.cpp:88), atan2 (environment_light.cpp:89),
- * sinf/cosf (sampler.cpp:23-25)) on n host arguments: fn 0 sin(a), 1 cos(a), 2 acos(a),
- * 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a) (float results widened to double). */
+ * sinf/cosf (sampler.cpp:23-25), and the microfacet BSDF's exp, log, erf, atan and tan
+ * (bsdf.cpp:45-96, bsdf.h:159-191)) on n host arguments: fn 0 sin(a), 1 cos(a), 2 acos(a),
+ * 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a) (float results widened to double), 6 exp(a),
+ * 7 log(a), 8 erf(a), 9 atan(a), 10 tan(a). */
 int rrt_libm_eval(rrt_ctx* ctx, int fn, const double* a, const double* b, double* out, uint64_t n);
 /* Run-time proof audit.  The renderer skips marches whose results its proofs
  * determine (camera-ray miss, shadow-ray occlusion, pixel and strip miss, Kerr occlusion); their

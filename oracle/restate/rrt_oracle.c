@@ -1305,7 +1305,12 @@ void ro_libm_eval(int fn, const double* a, const double* b, double* out, long n)
       case 2: out[k] = acos(a[k]); break;
       case 3: out[k] = atan2(a[k], b[k]); break;
       case 4: out[k] = sinf((float)a[k]); break;
-      default: out[k] = cosf((float)a[k]); break;
+      case 5: out[k] = cosf((float)a[k]); break;
+      case 6: out[k] = exp(a[k]); break;
+      case 7: out[k] = log(a[k]); break;
+      case 8: out[k] = erf(a[k]); break;
+      case 9: out[k] = atan(a[k]); break;
+      default: out[k] = tan(a[k]); break;
     }
   }
 }

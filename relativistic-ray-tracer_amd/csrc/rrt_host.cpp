@@ -1975,7 +1975,7 @@ extern "C" int rrt_tonemap_device(rrt_ctx* c, uint32_t n, const float* rgb, uint
 }
 
 extern "C" int rrt_libm_eval(rrt_ctx* c, int fn, const double* a, const double* b, double* out, uint64_t n) {
-  if (!c || !a || !out || fn < 0 || fn > 5 || (fn == 3 && !b)) return fail(c, RRT_E_INVALID, "bad argument");
+  if (!c || !a || !out || fn < 0 || fn > 10 || (fn == 3 && !b)) return fail(c, RRT_E_INVALID, "bad argument");
   if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "no device");
   if (n == 0) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));

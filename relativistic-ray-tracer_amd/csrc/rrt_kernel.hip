@@ -175,7 +175,8 @@ __global__ void rrt_tonemap_kernel(uint32_t n, const float* rgb, uint32_t* out, 
 
 // The device's restatements of the host C library's functions (rrt_glibm.h), evaluated on n
 // arguments: rrt_libm_eval checks them bit for bit against the host's libm (tests/test_gpu_glibm.py).
-// fn: 0 sin, 1 cos, 2 acos, 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a)
+// fn: 0 sin, 1 cos, 2 acos, 3 atan2(a, b), 4 sinf((float)a), 5 cosf((float)a), 6 exp, 7 log, 8 erf,
+// 9 atan, 10 tan
 __global__ void rrt_libm_kernel(int fn, uint64_t n, const double* a, const double* b, double* out) {
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
     const double x = a[k];
@@ -186,7 +187,12 @@ __global__ void rrt_libm_kernel(int fn, uint64_t n, const double* a, const doubl
       case 2: r = rrt_glibm_acos(x); break;
       case 3: r = rrt_glibm_atan2(x, b[k]); break;
       case 4: r = rrt_glibm_sinf((float)x); break;
-      default: r = rrt_glibm_cosf((float)x); break;
+      case 5: r = rrt_glibm_cosf((float)x); break;
+      case 6: r = rrt_glibm_exp(x); break;
+      case 7: r = rrt_glibm_log(x); break;
+      case 8: r = rrt_glibm_erf(x); break;
+      case 9: r = rrt_glibm_atan(x); break;
+      default: r = rrt_glibm_tan(x); break;
     }
     out[k] = r;
   }

@@ -394,7 +394,8 @@ class Renderer:
         d.width, d.height, d.texels = t.shape[1], t.shape[0], t.ctypes.data
         self._chk(lib().rrt_set_envmap(self.h, C.byref(d)))
 
-    LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5}
+    LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5, "exp": 6, "log": 7, "erf": 8,
+               "atan": 9, "tan": 10}
 
     def libm_eval(self, fn, a, b=None):
         """The device's restated host-libm function `fn` (rrt_glibm.h) on float64 arrays a (, b)."""

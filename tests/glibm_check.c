@@ -15,6 +15,9 @@
 //                   sinf, cosf (|x| < 120), half uniform in value, half log-uniform in magnitude,
 //                   and atan2 on random pairs and on the environment lookup's unit directions
 //   specials        zeros, infinities, NaNs, +-1 and the branch boundaries of every function
+//   mf K0 K1        the microfacet sampler (bsdf.cpp:76-86) on every Xi = k / RAND_MAX, k in
+//                   [K0, K1): log(1 - Xi), then for three roughnesses atan(sqrt(-a^2 log(1 - Xi))),
+//                   tan of that angle and exp(-tan^2 / a^2), each on the library's own inputs
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -32,12 +35,18 @@ static double (*volatile lib_acos)(double) = acos;
 static float (*volatile lib_sinf)(float) = sinf;
 static float (*volatile lib_cosf)(float) = cosf;
 static double (*volatile lib_atan2)(double, double) = atan2;
+static double (*volatile lib_exp)(double) = exp;
+static double (*volatile lib_log)(double) = log;
+static double (*volatile lib_erf)(double) = erf;
+static double (*volatile lib_atan)(double) = atan;
+static double (*volatile lib_tan)(double) = tan;
 
 static int same_d(double a, double b) { uint64_t x, y; memcpy(&x, &a, 8); memcpy(&y, &b, 8); return x == y || (a != a && b != b); }
 static int same_f(float a, float b) { uint32_t x, y; memcpy(&x, &a, 4); memcpy(&y, &b, 4); return x == y || (a != a && b != b); }
 
-enum { F_SIN, F_COS, F_ACOS, F_ACOSF, F_SINF, F_COSF, F_SINF_T, F_COSF_T, F_ATAN2, NF };
-static const char* names[NF] = {"sin", "cos", "acos", "acos_to_float", "sinf", "cosf", "sinf_theta", "cosf_theta", "atan2"};
+enum { F_SIN, F_COS, F_ACOS, F_ACOSF, F_SINF, F_COSF, F_SINF_T, F_COSF_T, F_ATAN2, F_EXP, F_LOG, F_ERF, F_ATAN, F_TAN, NF };
+static const char* names[NF] = {"sin", "cos", "acos", "acos_to_float", "sinf", "cosf", "sinf_theta", "cosf_theta", "atan2",
+                                "exp", "log", "erf", "atan", "tan"};
 static long long bad[NF], tested[NF];
 static double first_bad[NF];
 
@@ -145,11 +154,47 @@ int main(int argc, char** argv) {
           note(F_ACOS, same_d(rrt_glibm_acos(dy * r), lib_acos(dy * r)), dy * r);
         }
         note(F_ATAN2, same_d(rrt_glibm_atan2(ya, xa), lib_atan2(ya, xa)), ya);
+        // the microfacet functions: exp over its whole finite range and the subnormal results,
+        // log of any positive (subnormals included, sometimes near 1 or negative), erf, atan on
+        // the whole line, tan on the restated domain |x| <= 25
+        const double e = (splitmix(&s) & 1) ? rand_arg(&s, 760.0) : rand_arg(&s, 1.0);
+        note(F_EXP, same_d(rrt_glibm_exp(e), lib_exp(e)), e);
+        const uint64_t lr = splitmix(&s);
+        const double l = (lr & 3) == 0 ? 1.0 + rand_arg(&s, 0.1) : (lr & 31) == 1 ? -rand_arg(&s, 1e300) : fabs(rand_arg(&s, 1e308));
+        note(F_LOG, same_d(rrt_glibm_log(l), lib_log(l)), l);
+        const double ef = (splitmix(&s) & 1) ? rand_arg(&s, 7.0) : rand_arg(&s, 1e300);
+        note(F_ERF, same_d(rrt_glibm_erf(ef), lib_erf(ef)), ef);
+        const double at = (splitmix(&s) & 1) ? rand_arg(&s, 20.0) : rand_arg(&s, 1e300);
+        note(F_ATAN, same_d(rrt_glibm_atan(at), lib_atan(at)), at);
+        const double tn = (splitmix(&s) & 1) ? rand_arg(&s, 3.2) : rand_arg(&s, 25.0);
+        note(F_TAN, same_d(rrt_glibm_tan(tn), lib_tan(tn)), tn);
         tested[F_SIN]++; tested[F_COS]++; tested[F_ACOS]++; tested[F_SINF]++; tested[F_COSF]++;
-        tested[F_ATAN2]++;
+        tested[F_ATAN2]++; tested[F_EXP]++; tested[F_LOG]++; tested[F_ERF]++; tested[F_ATAN]++; tested[F_TAN]++;
       }
     }
     report("random");
+  } else if (!strcmp(argv[1], "mf") && argc == 4) {
+    const long long k0 = atoll(argv[2]), k1 = atoll(argv[3]);
+    static const double alphas[3] = {0.05, 0.25, 0.5};
+#pragma omp parallel for schedule(static, 65536) reduction(+ : tested[:NF])
+    for (long long k = k0; k < k1; ++k) {
+      const double xi = ((double)(int)k) / 2147483647.0;
+      const double lg = lib_log(1 - xi);                      // bsdf.cpp:78
+      note(F_LOG, same_d(rrt_glibm_log(1 - xi), lg), 1 - xi);
+      tested[F_LOG]++;
+      for (int a = 0; a < 3; ++a) {
+        const double a2 = alphas[a] * alphas[a];
+        const double q = sqrt(-a2 * lg);
+        const double th = lib_atan(q);                        // theta_h
+        note(F_ATAN, same_d(rrt_glibm_atan(q), th), q);
+        const double t = lib_tan(th);                         // bsdf.cpp:83
+        note(F_TAN, same_d(rrt_glibm_tan(th), t), th);
+        const double ea = -t * t / a2;                        // bsdf.cpp:84
+        note(F_EXP, same_d(rrt_glibm_exp(ea), lib_exp(ea)), ea);
+        tested[F_ATAN]++; tested[F_TAN]++; tested[F_EXP]++;
+      }
+    }
+    report("mf");
   } else if (!strcmp(argv[1], "specials")) {
     // every branch boundary of the restated routines (high words from s_sin.c, e_asin.c,
     // e_atan2.c, s_sinf.c), 64 ulps either side, both signs, plus zeros, infinities, NaNs
@@ -170,6 +215,34 @@ int main(int argc, char** argv) {
     const double extra[] = {0.0, -0.0, INFINITY, -INFINITY, NAN, 1.0, -1.0, 0.126, -0.126, 0.0625,
                             3.14159265358979323, 1.5707963267948966, 2.426265, 105414350.0};
     for (unsigned i = 0; i < sizeof(extra) / sizeof(extra[0]); ++i) pts[np++] = extra[i];
+    // the microfacet functions' branch boundaries (e_exp.c, e_log.c, s_erf.c, s_atan.c, s_tan.c)
+    static const uint32_t mhis[] = {0x3c900000u, 0x40800000u, 0x40900000u, 0x40862e42u, 0x408633ceu, 0x40874910u,
+                                    0x3fee0000u, 0x3ff10900u, 0x3fe60000u, 0x00100000u, 0x000fffffu, 0x3e300000u,
+                                    0x3feb0000u, 0x3ff40000u, 0x4006db6eu, 0x40180000u, 0x00800000u, 0x3e4bb67au,
+                                    0x3fb00000u, 0x40300000u, 0x43349ff2u, 0x3e4b096cu, 0x3faf212du, 0x3fe92f1au,
+                                    0x40390000u, 0x3ff921fbu, 0x400921fbu, 0x4012d97cu};
+    double mpts[2 * 28 * 129];
+    int nm = 0;
+    for (unsigned h = 0; h < sizeof(mhis) / sizeof(mhis[0]); ++h)
+      for (int d = -64; d <= 64; ++d) {
+        const uint64_t b = ((uint64_t)mhis[h] << 32) + (uint64_t)(int64_t)d;
+        double v;
+        memcpy(&v, &b, 8);
+        mpts[nm++] = v;
+        mpts[nm++] = -v;
+      }
+    for (int i = 0; i < nm + np; ++i) {
+      const double x = i < nm ? mpts[i] : pts[i - nm];
+      note(F_EXP, same_d(rrt_glibm_exp(x), lib_exp(x)), x);
+      note(F_LOG, same_d(rrt_glibm_log(x), lib_log(x)), x);
+      note(F_ERF, same_d(rrt_glibm_erf(x), lib_erf(x)), x);
+      note(F_ATAN, same_d(rrt_glibm_atan(x), lib_atan(x)), x);
+      tested[F_EXP]++; tested[F_LOG]++; tested[F_ERF]++; tested[F_ATAN]++;
+      if (fabs(x) <= 25.0 || x != x || isinf(x)) {
+        note(F_TAN, same_d(rrt_glibm_tan(x), lib_tan(x)), x);
+        tested[F_TAN]++;
+      }
+    }
     for (int i = 0; i < np; ++i) {
       const double x = pts[i];
       note(F_SIN, same_d(rrt_glibm_sin(x), lib_sin(x)), x);

@@ -108,13 +108,12 @@ class Case:
 
     @property
     def exact(self):
-        """Cases the GPU must match bit for bit: every case whose scene has no microfacet BSDF.
-        The per-sample sin/cos (bounces, environment light), acos/atan2 (environment light,
-        hemisphere sampler) and sinf/cosf (hemisphere sampler) are the host C library's own
-        routines restated on the device (csrc/rrt_glibm.h, tests/test_glibm.py); the microfacet
-        BSDF's tan/exp/log/atan/erf (bsdf.cpp:45-96, bsdf.h:159-191) still use the device libm, and
-        those cases are held to the north-star per-pixel bound instead."""
-        return "microfacet" not in self.info.get("dae", "")
+        """Cases the GPU must match bit for bit: every case.  The per-sample transcendentals are the
+        host C library's own routines restated on the device (csrc/rrt_glibm.h, tests/test_glibm.py):
+        sin/cos (bounces, environment light), acos/atan2 (environment light, hemisphere sampler),
+        sinf/cosf (hemisphere sampler) and, since round 5, the microfacet BSDF's exp, log, erf, atan
+        and tan (bsdf.cpp:45-96, bsdf.h:159-191)."""
+        return True
 
 
 def all_cases():

@@ -191,7 +191,8 @@ def render(scene, cam, params, x0, y0, w, h, threads=None, counters=False):
     return rgb, cnt, draws, ctr
 
 
-LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5}
+LIBM_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "sinf": 4, "cosf": 5, "exp": 6, "log": 7, "erf": 8, "atan": 9,
+           "tan": 10}
 
 
 def libm_eval(fn, a, b=None):

@@ -3,11 +3,14 @@ library itself, on the CPU: the same source compiled as C must return the librar
 
 The reference calls glibc's sin/cos (sampler.cpp:53-55 cosine-weighted hemisphere sampler of every
 diffuse bounce; environment_light.cpp:97-137), acos (sampler.cpp:20, bsdf.h:166,
-environment_light.cpp:88), atan2 (environment_light.cpp:89) and sinf/cosf (sampler.cpp:23-25).
+environment_light.cpp:88), atan2 (environment_light.cpp:89), sinf/cosf (sampler.cpp:23-25) and, in
+the microfacet BSDF, exp, log, erf, atan and tan (bsdf.cpp:45-96, bsdf.h:159-191).
 Checked here (tests/glibm_check.c):
   * every argument the samplers can produce: Xi = k / RAND_MAX for all 2^31 k, through
     cos/sin(2 PI Xi), acos(Xi), (float)acos(Xi) and sinf/cosf of (float)acos(Xi), (float)(2 PI Xi);
   * sinf and cosf on every float of the restated domain |x| < 120;
+  * the microfacet sampler's chain on all 2^31 Xi: log(1 - Xi), atan(sqrt(-a^2 log(1 - Xi))), tan of
+    it and exp(-tan^2 / a^2) for three roughnesses;
   * 10^8 random arguments per function (value- and log-uniform; atan2 also on unit directions);
   * every branch boundary, zeros, infinities and NaNs.
 The GPU side of the same check is tests/test_gpu_glibm.py.
@@ -103,3 +106,9 @@ def test_every_sampler_argument(checker):
     """All 2^31 values random_uniform() can return, through each reference call site."""
     res = run(checker, "sampler", 0, 2 ** 31)
     assert res["cos"][0] == 2 ** 31
+
+
+def test_every_microfacet_sampler_argument(checker):
+    """bsdf.cpp:76-86 on all 2^31 values random_uniform() can return, three roughnesses."""
+    res = run(checker, "mf", 0, 2 ** 31)
+    assert res["log"][0] == 2 ** 31 and res["tan"][0] == 3 * 2 ** 31

@@ -7,7 +7,9 @@ random_uniform() can return, taken through each reference call site (cos/sin(2 P
 sampler.cpp:53-55; acos(Xi), sampler.cpp:20; sinf/cosf of (float)acos(Xi) and (float)(2 PI Xi),
 sampler.cpp:23-25), random arguments over each restated domain, the environment light's
 atan2(-u.z, u.x) / acos(u.y) on random unit directions (environment_light.cpp:88-89), and every
-branch boundary.  tests/test_glibm.py runs the full domains on the CPU build of the same source."""
+branch boundary; and the microfacet BSDF's exp, log, erf, atan and tan (bsdf.cpp:45-96,
+bsdf.h:159-191) on its sampler's arguments and on random arguments over each restated domain.
+tests/test_glibm.py runs the full domains on the CPU build of the same source."""
 import numpy as np
 import pytest
 
@@ -105,3 +107,51 @@ def test_branch_boundaries_and_specials(gpu):
     check(gpu, "cosf", f)
     yy, xx = np.meshgrid(b, b[::5])
     check(gpu, "atan2", yy.ravel(), xx.ravel())
+
+
+def test_microfacet_functions(gpu):
+    """The microfacet sampler's chain on a 2^24 stride through random_uniform()'s values (bsdf.cpp:76-86:
+    log(1 - Xi), atan(sqrt(-a^2 log(1 - Xi))), tan of it, exp(-tan^2 / a^2)), each on the library's own
+    inputs; then random arguments: exp over its finite range (subnormal results included), log of any
+    positive double and near 1, erf, atan on the whole line, tan on its restated domain |x| <= 25."""
+    k = np.arange(0, 2 ** 31, 128, dtype=np.int64) + np.random.default_rng(2).integers(0, 128, 2 ** 24)
+    xi = k.astype(np.float64) / 2147483647.0
+    check(gpu, "log", 1 - xi)
+    lg = ol.libm_eval("log", 1 - xi)
+    for alpha in (0.05, 0.25, 0.5):
+        a2 = alpha * alpha
+        q = np.sqrt(-a2 * lg)
+        check(gpu, "atan", q)
+        th = ol.libm_eval("atan", q)
+        check(gpu, "tan", th)
+        t = ol.libm_eval("tan", th)
+        check(gpu, "exp", -t * t / a2)
+    g = np.random.default_rng(20261018)
+    n = 1 << 22
+
+    def mixed(lim, octaves=60):
+        v = g.uniform(-lim, lim, n)
+        e = g.uniform(np.log2(lim) - octaves, np.log2(lim), n)
+        v[: n // 2] = np.sign(g.uniform(-1, 1, n // 2)) * 2.0 ** e[: n // 2]
+        return v
+
+    check(gpu, "exp", mixed(760.0))
+    check(gpu, "exp", mixed(1.0))
+    check(gpu, "log", np.abs(mixed(1e308, 2000)))
+    check(gpu, "log", 1.0 + mixed(0.1))
+    check(gpu, "erf", mixed(7.0))
+    check(gpu, "atan", mixed(20.0))
+    check(gpu, "atan", mixed(1e300))
+    check(gpu, "tan", mixed(3.2))
+    check(gpu, "tan", mixed(25.0))
+    b = boundaries()
+    mb = np.array([(h << 32) + d for h in (0x3C900000, 0x40800000, 0x40900000, 0x40862E42, 0x408633CE, 0x40874910,
+                                             0x3FEE0000, 0x3FF10900, 0x3FE60000, 0x00100000, 0x000FFFFF, 0x3E300000,
+                                             0x3FEB0000, 0x3FF40000, 0x4006DB6E, 0x40180000, 0x00800000, 0x3E4BB67A,
+                                             0x3FB00000, 0x40300000, 0x43349FF2, 0x3E4B096C, 0x3FAF212D, 0x3FE92F1A,
+                                             0x40390000, 0x3FF921FB, 0x400921FB, 0x4012D97C)
+                   for d in range(-64, 65)], np.uint64).view(np.float64)
+    pts = np.concatenate([b, mb, -mb])
+    for fn in ("exp", "log", "erf", "atan"):
+        check(gpu, fn, pts)
+    check(gpu, "tan", pts[~(np.abs(pts) > 25)])
