@@ -130,7 +130,7 @@ def test_microfacet_functions(gpu):
     n = 1 << 22
 
     def mixed(lim, octaves=60):
-        v = g.uniform(-lim, lim, n)
+        v = g.uniform(-1.0, 1.0, n) * lim
         e = g.uniform(np.log2(lim) - octaves, np.log2(lim), n)
         v[: n // 2] = np.sign(g.uniform(-1, 1, n // 2)) * 2.0 ** e[: n // 2]
         return v
