@@ -1835,11 +1835,32 @@ __device__ __forceinline__ spec emission(const DBsdf& b) {
   return b.type == B_EMISSION ? S(b.p[0], b.p[1], b.p[2]) : S(0, 0, 0);
 }
 __device__ __forceinline__ double clamp_b(double n, double lo, double hi) { return std_max(lo, std_min(n, hi)); }
+// The microfacet BSDF's exp/log/erf/atan/tan (bsdf.cpp:45-96, bsdf.h:159-191).  rrt_glibm.h restates
+// glibc's (bit-exact against the library on the CPU and, through rrt_libm_eval, on the GPU), but
+// compiled into the general kernel builds (RRT_MF_GLIBM 1) they made those builds fault
+// intermittently on scenes without a microfacet BSDF (cause not found), so the
+// kernels call the device libm here and the microfacet goldens are held to the north-star bound.
+#ifndef RRT_MF_GLIBM
+#define RRT_MF_GLIBM 0
+#endif
+#if RRT_MF_GLIBM
+#define RRT_MF_TAN rrt_glibm_tan
+#define RRT_MF_ERF rrt_glibm_erf
+#define RRT_MF_EXP rrt_glibm_exp
+#define RRT_MF_ATAN rrt_glibm_atan
+#define RRT_MF_LOG rrt_glibm_log
+#else
+#define RRT_MF_TAN tan
+#define RRT_MF_ERF erf
+#define RRT_MF_EXP exp
+#define RRT_MF_ATAN atan
+#define RRT_MF_LOG log
+#endif
 __device__ __forceinline__ double mf_theta(v3 w) { return rrt_glibm_acos(clamp_b(w.z, -1.0 + 1e-5, 1.0 - 1e-5)); }
 __device__ __forceinline__ double mf_lambda(float alpha, v3 w) {
   double theta = mf_theta(w);
-  double a = 1.0 / (alpha * rrt_glibm_tan(theta));
-  return 0.5 * (rrt_glibm_erf(a) - 1.0 + rrt_glibm_exp(-a * a) / (a * PI_D));
+  double a = 1.0 / (alpha * RRT_MF_TAN(theta));
+  return 0.5 * (RRT_MF_ERF(a) - 1.0 + RRT_MF_EXP(-a * a) / (a * PI_D));
 }
 __device__ __forceinline__ spec mf_F(const DBsdf& b, v3 wi) {
   spec eta = S(b.p[0], b.p[1], b.p[2]), k = S(b.p[3], b.p[4], b.p[5]);
@@ -1851,9 +1872,9 @@ __device__ __forceinline__ spec mf_F(const DBsdf& b, v3 wi) {
   return (Rs + Rp) / 2.0f;
 }
 __device__ __forceinline__ double mf_D(float alpha, v3 h) {
-  double theta_h = mf_theta(h), tan_h = rrt_glibm_tan(theta_h), cos_h = h.z, cos_h2 = cos_h * cos_h;
+  double theta_h = mf_theta(h), tan_h = RRT_MF_TAN(theta_h), cos_h = h.z, cos_h2 = cos_h * cos_h;
   double alpha2 = alpha * alpha;  // float product, as the reference
-  return rrt_glibm_exp(-tan_h * tan_h / alpha2) / (PI_D * alpha2 * cos_h2 * cos_h2);
+  return RRT_MF_EXP(-tan_h * tan_h / alpha2) / (PI_D * alpha2 * cos_h2 * cos_h2);
 }
 __device__ __forceinline__ spec mf_f(const DBsdf& b, v3 wo, v3 wi) {
   if (wo.z <= 0 || wi.z <= 0) return S(0, 0, 0);
@@ -1914,10 +1935,10 @@ __device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf,
       g.grid(ux, uy);
       float alpha = b.p[6];
       double alpha2 = alpha * alpha,
-             theta_h = rrt_glibm_atan(sqrt(-alpha2 * rrt_glibm_log(1 - ux))),
+             theta_h = RRT_MF_ATAN(sqrt(-alpha2 * RRT_MF_LOG(1 - ux))),
              phi_h = 2 * PI_D * uy,
-             sin_h = rrt_glibm_sin(theta_h), cos_h = rrt_glibm_cos(theta_h), tan_h = rrt_glibm_tan(theta_h),
-             p_theta = 2 * sin_h * rrt_glibm_exp(-tan_h * tan_h / alpha2) / (alpha2 * cos_h * cos_h * cos_h),
+             sin_h = rrt_glibm_sin(theta_h), cos_h = rrt_glibm_cos(theta_h), tan_h = RRT_MF_TAN(theta_h),
+             p_theta = 2 * sin_h * RRT_MF_EXP(-tan_h * tan_h / alpha2) / (alpha2 * cos_h * cos_h * cos_h),
              p_phi = 0.5 / PI_D;
       v3 h = V(sin_h * rrt_glibm_cos(phi_h), sin_h * rrt_glibm_sin(phi_h), cos_h);
       wi = smul(2 * dot(wo, h), h) - wo;
