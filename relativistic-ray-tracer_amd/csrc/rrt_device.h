@@ -741,7 +741,8 @@ __device__ __forceinline__ void next_micro(const DHole& h, v3& o, v3& d, double&
 // Schwarzschild march below and the Kerr march (query_kerr).
 // any_rt: a shadow query chosen at run time (the path pool kernel's rays share one query call)
 // The walk of a segment that passed the skips (segment_query); cell: its start's grid cell or -1.
-template <bool ANY, bool COUNT>
+// W4: the 4-wide walk may run (query's W4; the Kerr march walks the binary tree only)
+template <bool ANY, bool COUNT, bool W4 = true>
 __device__ __forceinline__ bool segment_walk(const KParams& kp, v3 o, v3 d, double max_t, v3 e, int cell,
                                              Isect* is, Counters& cn, bool any_rt = false) {
   // oversized leaves with no primitive within reach of a short segment are not offered
@@ -764,10 +765,10 @@ __device__ __forceinline__ bool segment_walk(const KParams& kp, v3 o, v3 d, doub
   RRT_T0(tt0);
   bool hit;
   if (!COUNT) {  // the search tree (4 wide, else binary; or, for A/B, the clean tree or the reference tree)
-    const int r4 = kp.free4 ? traverse_free4<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt) : 2;
+    const int r4 = (W4 && kp.free4) ? traverse_free4<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt) : 2;
     hit = r4 == 2 ? traverse_free<ANY, false>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask, any_rt) : r4 == 1;
   } else if (kp.count_exec) {
-    const int r4 = kp.free4 ? traverse_free4<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask) : 2;
+    const int r4 = (W4 && kp.free4) ? traverse_free4<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask) : 2;
     hit = r4 == 2 ? traverse_free<ANY, true>(kp, o, d, y, seg_t, slot, b1, b2, cn, !fast, bmask) : r4 == 1;
   }
   else
@@ -795,7 +796,7 @@ __device__ __forceinline__ bool segment_walk(const KParams& kp, v3 o, v3 d, doub
   }
   return true;
 }
-template <bool ANY, bool COUNT>
+template <bool ANY, bool COUNT, bool W4 = true>
 __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, double max_t, v3 e, Isect* is,
                                               Counters& cn, bool any_rt = false) {
   // e = o + d * max_t.  COUNT && kp.count_exec: count the work this path executes (grid / root
@@ -804,7 +805,7 @@ __device__ __forceinline__ bool segment_query(const KParams& kp, v3 o, v3 d, dou
   if (opt && segment_outside_root(kp, o, e)) return false;  // root test fails
   const int cell = opt ? grid_cell(kp.grid, o) : -1;
   if (cell_clear(kp.grid, cell, max_t)) return false;  // no primitive within reach
-  return segment_walk<ANY, COUNT>(kp, o, d, max_t, e, cell, is, cn, any_rt);
+  return segment_walk<ANY, COUNT, W4>(kp, o, d, max_t, e, cell, is, cn, any_rt);
 }
 
 // ------------------------------------------------------------------ kernel variants
@@ -1022,7 +1023,7 @@ __device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect*
     const double max_t = norm(seg);
     const double inv = xdiv(1., max_t);
     const v3 sd = V(seg.x * inv, seg.y * inv, seg.z * inv);  // normalize(seg), norm shared
-    if (segment_query<ANY, COUNT>(kp, a, sd, max_t, a + vmul(sd, max_t), is, cn)) return true;
+    if (segment_query<ANY, COUNT, false>(kp, a, sd, max_t, a + vmul(sd, max_t), is, cn)) return true;
     a = b;
   }
   return false;
@@ -1398,7 +1399,10 @@ __device__ __forceinline__ bool camera_hit_proof(const KParams& kp, v3 o, v3 d, 
                         // query too large for the inliner)
 #define RRT_QUERY_ATTR __device__ __forceinline__
 #endif
-template <bool ANY, bool COUNT, bool KERR = false>
+// W4: walks may take the 4-wide search tree -- the LEAN builds' choice; the general and Kerr builds
+// walk the binary tree (with the 4-wide walk inlined their scratch grew 2.5-3x: general batch kernel
+// 592 -> 1488 B/lane, Kerr 720 -> 2304 and cfg5 1.41 -> 3.76 s per frame, profiles/r05_ab_kerr_bvh4.txt)
+template <bool ANY, bool COUNT, bool KERR = false, bool W4 = true>
 RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn, bool any_rt = false) {
   if (KERR) return query_kerr<ANY, COUNT>(kp, o, d, is, cn);
   if (COUNT && !kp.count_exec && !(kp.diag & 2)) cn.query++;
@@ -1433,7 +1437,7 @@ RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn
         break;
       }
       if (!walk) break;
-      if (segment_walk<ANY, false>(kp, o, d, max_t, e, cell, is, cn, any_rt)) {
+      if (segment_walk<ANY, false, W4>(kp, o, d, max_t, e, cell, is, cn, any_rt)) {
         RRT_QACC(tq0);
         return true;
       }
@@ -1454,7 +1458,7 @@ RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn
       return false;
     }
     e = o + vmul(d, max_t);
-    if (segment_query<ANY, COUNT>(kp, o, d, max_t, e, is, cn, any_rt)) {
+    if (segment_query<ANY, COUNT, W4>(kp, o, d, max_t, e, is, cn, any_rt)) {
       RRT_QACC(tq0);
       return true;
     }
@@ -1775,10 +1779,10 @@ __device__ __forceinline__ bool pixel_heavy(const KParams& kp, uint32_t px, uint
 
 // query() behind a call: the caller keeps only what is live across the call, the walk gets the
 // register file to itself (rrt_sample.hip batch kernel)
-template <bool ANY, bool KERR>
+template <bool ANY, bool KERR, bool W4 = true>
 __device__ __noinline__ bool query_call(const KParams& kp, v3 o, v3 d, Isect* is) {
   Counters cn = {};
-  return query<ANY, false, KERR>(kp, o, d, is, cn);
+  return query<ANY, false, KERR, W4>(kp, o, d, is, cn);
 }
 // The occlusion proof's build tag W (0: no proof in this build).  Its out-of-line parts (the
 // face test, or the whole proof in mode 1) get one copy per calling kernel build: a callee shared
@@ -1791,7 +1795,7 @@ __device__ __noinline__ bool shadow_proof_call(const KParams& kp, v3 o, v3 d) {
   return shadow_occluded_proof(kp, o, d, kp.hole.steps);
 }
 // W: the occlusion proof's build tag (0: none)
-template <bool ANY, bool COUNT, bool NI, bool KERR = false, int W = 0>
+template <bool ANY, bool COUNT, bool NI, bool KERR = false, int W = 0, bool W4 = true>
 __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   // shadow rays: the occlusion proof first (Schwarzschild; never in the reference-work counts)
   if (RRT_SHADOW_PROOF && W && ANY && !KERR && kp.occ.on && !(COUNT && !kp.count_exec)) {
@@ -1807,8 +1811,8 @@ __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* i
       return true;
     }
   }
-  if (NI && !COUNT) return query_call<ANY, KERR>(kp, o, d, is);
-  return query<ANY, COUNT, KERR>(kp, o, d, is, cn);
+  if (NI && !COUNT) return query_call<ANY, KERR, W4>(kp, o, d, is);
+  return query<ANY, COUNT, KERR, W4>(kp, o, d, is, cn);
 }
 
 // ------------------------------------------------------------------ BSDFs (bsdf.cpp / bsdf.h)

@@ -11,7 +11,7 @@ namespace rrt {
 // `trace` = the geodesic-marched BVH query; DEEP (bounce) builds and depth <= 1 builds share it.
 template <bool ANY, bool COUNT, bool DEEP, int LEAN>
 __device__ __forceinline__ bool trace(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
-  return query<ANY, COUNT, LEAN == V_KERR>(kp, o, d, is, cn);
+  return query<ANY, COUNT, LEAN == V_KERR, is_lean(LEAN)>(kp, o, d, is, cn);
 }
 
 // LEAN: area/point lights only, no microfacet BSDF.  The shading frame is rebuilt per light sample

@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_path_kernel(const KParams* __r
         h = shadow_occluded_proof<RRT_OCC_TAG_PATH(WAVES)>(kp, o, d, kp.hole.steps);
         known = h;
       }
-      if (!known) h = query<false, false, false>(kp, o, d, &is, cn, any);
+      if (!known) h = query<false, false, false, false>(kp, o, d, &is, cn, any);
       const uint32_t q = wb + rp;
       if (rs1) {
         pput(pl.res1, q, (uint8_t)(h ? 1u : 0u));

@@ -70,7 +70,7 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
       // only the loop state and the RNG stay in registers across the shadow query
       lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
-      if (!query_nx<true, COUNT, NI, LEAN == V_KERR, W>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
+      if (!query_nx<true, COUNT, NI, LEAN == V_KERR, W, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
         L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
     }
   }
@@ -98,7 +98,7 @@ __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl
     const v3 wi_world = to_world(f, w_in);
     const spec fw = bsdf_f(kp.bsdfs[bsdf], to_local(f, wo), w_in);
     Isect is2;
-    if (query_nx<false, COUNT, NI, LEAN == V_KERR>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (query_nx<false, COUNT, NI, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * fw) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
       const v3 wd = unit(w);
       bool hitq = false;
       if (!camera_proven_miss<COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
-          query<false, COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
+          query<false, COUNT, LEAN == V_KERR, is_lean(LEAN)>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
         hitq = true;
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
       if (COUNT && aud) {  // the pixel pass's proofs say this camera ray misses
         Counters c2 = {};
         Isect i2;
-        const bool ex = query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &i2, c2);
+        const bool ex = query<false, false, LEAN == V_KERR, is_lean(LEAN)>(kp, ld3(cam.pos), wd, &i2, c2);
         if (aud & 1u) audit_note(kp, RRT_AUDIT_PIXEL, ex);
         if (aud & 2u) audit_note(kp, RRT_AUDIT_STRIP, ex);
       }
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         is->bsdf = (int)RRT_ZERO_BSDF;  // a hit whose radiance is +0: no record, no shading
         return true;
       }
-      return query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR>(kp, ld3(cam.pos), wd, is, cn);
+      return query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, is, cn);
     };
     const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;  // this group's lanes
     const uint64_t lt = ((1ull << lane) - 1ull) & gmask;                         // group lanes before me
@@ -1363,7 +1363,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_first_kernel(const KParams* __
     Isect is;
     const v3 wd = unit(w);
     const bool hit = !camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
-                     query<false, false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, &is, cn);
+                     query<false, false, LEAN == V_KERR, is_lean(LEAN)>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (!hit && !is_lean(LEAN) && kp.env.w) s = env_dir(kp.env, unit(w));
     if (hit) {
