@@ -983,9 +983,16 @@ __device__ __forceinline__ void audit_note(const KParams& kp, int k, bool violat
 __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d);
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn);
+template <bool COUNT>
+__device__ __forceinline__ bool kerr_shadow(const KParams& kp, v3 o, v3 d, Counters& cn);
+#ifndef RRT_KERR_SHADOW_LOOP
+#define RRT_KERR_SHADOW_LOOP 0  // 1: the proof's coarse march and the exact march in one loop (A/B, kerr_shadow)
+#endif
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   // shadow rays: the occlusion proof first (never in the reference-work counts)
+  if (RRT_KERR_SHADOW_LOOP && !RRT_LIBM_DIVSQRT && ANY && kp.kproof.on && !(COUNT && !kp.count_exec))
+    return kerr_shadow<COUNT>(kp, o, d, cn);
   if (ANY && kp.kproof.on && !(COUNT && !kp.count_exec) && kerr_occluded_proof(kp, o, d)) {
     if (COUNT && kp.audit && audit_pick(kp, o, d)) {
       Counters c2 = {};
@@ -1135,21 +1142,23 @@ __device__ __forceinline__ int occ_exit_quad(const KParams& kp, v3 a, v3 b, doub
   }
   return out ? -1 : 0;
 }
+// A ray whose straight line leaves the room through a face without wall pieces (the open side of a
+// Cornell box) almost never ends on a wall: spare it the coarse march (false: no proof)
+__device__ __forceinline__ bool kerr_proof_worth(const KParams& kp, v3 o, v3 d) {
+  double te = 1e300;
+  int fe = -1;
+  for (int k = 0; k < 3; ++k) {
+    const double dk = k == 0 ? d.x : k == 1 ? d.y : d.z, ok = k == 0 ? o.x : k == 1 ? o.y : o.z;
+    if (dk == 0.0) continue;
+    const double t = ((dk > 0.0 ? kp.miss.hi[k] : kp.miss.lo[k]) - ok) / dk;
+    if (t < te) { te = t; fe = dk > 0.0 ? k + 3 : k; }
+  }
+  return !(fe >= 0 && kp.kproof.nq[fe] == 0);
+}
 __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d) {
   const DHole& h = kp.hole;
   const DKerrProof& kq = kp.kproof;
-  {  // a ray whose straight line leaves the room through a face without wall pieces (the open side
-     // of a Cornell box) almost never ends on a wall: spare it the coarse march
-    double te = 1e300;
-    int fe = -1;
-    for (int k = 0; k < 3; ++k) {
-      const double dk = k == 0 ? d.x : k == 1 ? d.y : d.z, ok = k == 0 ? o.x : k == 1 ? o.y : o.z;
-      if (dk == 0.0) continue;
-      const double t = ((dk > 0.0 ? kp.miss.hi[k] : kp.miss.lo[k]) - ok) / dk;
-      if (t < te) { te = t; fe = dk > 0.0 ? k + 3 : k; }
-    }
-    if (fe >= 0 && kq.nq[fe] == 0) return false;
-  }
+  if (!kerr_proof_worth(kp, o, d)) return false;
   v3 q, p;
   kerr_init(h, o, d, q, p);
   if (!(norm2(q) > kq.r_near2)) return false;  // starting near the hole
@@ -1186,6 +1195,98 @@ __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 
     a = b;
   }
   return false;
+}
+// Kerr shadow query in one loop (query_kerr with the proof on): the occlusion proof's coarse march
+// and, when it gives no proof, the exact march from the start, as one sequence of RK4 steps per
+// lane.  Run as two loops, a wave spends the longest coarse march of its lanes and then their
+// longest exact march; here a lane leaving the proof starts its exact march at the next step, so
+// the wave runs the longest coarse + exact sequence of any one lane, and lanes in either mode share
+// the step's four Hamiltonian evaluations.  Each mode's steps, tests and results are those of
+// kerr_occluded_proof and kerr_march (the exact step's stretch is 1: (dt r) * 1 is dt r exactly).
+template <bool COUNT>
+__device__ __forceinline__ bool kerr_shadow(const KParams& kp, v3 o, v3 d, Counters& cn) {
+  const DHole& h = kp.hole;
+  const DKerrProof& kq = kp.kproof;
+  const double rh2 = h.r_hor * h.r_hor;
+  const v3 c = ld3(h.c);
+  v3 q, p;
+  kerr_init(h, o, d, q, p);
+  bool coarse = kerr_proof_worth(kp, o, d) && norm2(q) > kq.r_near2;
+  v3 a = o, a0 = o;  // the chord's (segment's) start; the proof's previous chord start
+  bool a_in = occ_inside(kp.occ, a);
+  double swept = 0.0;
+  int j = 0;
+  bool restart = false;  // the proof gave up: the exact march starts from the ray at the next step
+#pragma unroll 1
+  for (;;) {
+    if (restart) {
+      restart = false;
+      coarse = false;
+      kerr_init(h, o, d, q, p);
+      a = o; swept = 0.0; j = 0;
+    }
+    if (coarse ? !(j < kq.max_steps) : !(j < h.kerr_max_steps && swept < 2.0 * PI_D)) {
+      if (!coarse) return false;
+      restart = true;
+      continue;
+    }
+    v3 q1 = q, p1 = p;
+    double sw1 = swept;
+    KArith<true> fast;
+    bool escaped = kerr_advance(h, q1, p1, sw1, fast, coarse ? kq.stretch : 1.0);
+    if (__builtin_expect(!fast.ok, 0)) {
+      if (coarse) { restart = true; continue; }
+      KArith<false> ieee;  // the exact march's step with an operand outside the cores' range
+      q1 = q; p1 = p; sw1 = swept;
+      escaped = kerr_advance(h, q1, p1, sw1, ieee);
+    }
+    if (coarse) {  // kerr_occluded_proof's step
+      if (escaped || !(sw1 < kq.swept_max) || !(norm2(q1) > kq.r_near2)) { restart = true; continue; }
+      q = q1; p = p1; swept = sw1;
+      const v3 b = kerr_world(h, q);
+      {
+        const v3 u = b - a, w = c - a;
+        const double uu = norm2(u), t = uu > 0.0 ? fmin(fmax(dot(u, w) / uu, 0.0), 1.0) : 0.0;
+        if (!(norm2(w - vmul(u, t)) > kq.r_near2)) { restart = true; continue; }
+      }
+      const bool b_in = occ_inside(kp.occ, b);
+      if (!b_in || !a_in) {
+        int res = occ_exit_quad(kp, a, b, kq.delta);
+        if (res <= 0 && j > 0) {
+          const v3 u = b - a0, w = a - a0;
+          const double uu = norm2(u), uw = dot(u, w);
+          const double beta = sqrt(fmax(norm2(w) - uw * uw / uu, 0.0)) * (1.0 + 1e-6);
+          if (uu > 0.0 && occ_exit_quad(kp, a0, b, kq.delta + beta) > 0) res = 1;
+        }
+        if (res > 0) {
+          if (COUNT && kp.audit && audit_pick(kp, o, d)) {
+            Counters c2 = {};
+            audit_note(kp, RRT_AUDIT_KERR, !kerr_march<true, false>(kp, o, d, nullptr, c2));
+          }
+          return true;
+        }
+        if (res < 0) { restart = true; continue; }
+      }
+      a_in = b_in;
+      a0 = a;
+      a = b;
+      ++j;
+      continue;
+    }
+    // kerr_march's step
+    if (escaped) return false;
+    q = q1; p = p1; swept = sw1;
+    if (COUNT) cn.micro++;
+    if (kerr_r2(h, q) <= rh2) return false;  // captured
+    const v3 b = kerr_world(h, q);
+    const v3 seg = b - a;
+    const double max_t = norm(seg);
+    const double inv = xdiv(1., max_t);
+    const v3 sd = V(seg.x * inv, seg.y * inv, seg.z * inv);
+    if (segment_query<true, COUNT, false>(kp, a, sd, max_t, a + vmul(sd, max_t), nullptr, cn)) return true;
+    a = b;
+    ++j;
+  }
 }
 // The whole march by the recurrence, step 0 included: the ray (o, d) is the state of a step from
 // the point A = o itself (|A - c| = 1 / u, so v_prev = rho u, E_prev = x, s_prev chosen so the

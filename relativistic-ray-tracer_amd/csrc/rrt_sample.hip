@@ -561,6 +561,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 #ifndef RRT_BATCH_CALL
 #define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
 #endif
+#ifndef RRT_KERR_CALL
+#define RRT_KERR_CALL 0  // 1: the Kerr build's queries out of line in the batch kernel (register A/B)
+#endif
+#define RRT_BCALL(LEAN) (RRT_BATCH_CALL || ((LEAN) == V_KERR && RRT_KERR_CALL))
 
 // draw-offset slots per group and step: a hit takes Dh / Dm slots (2 with one area light, the
 // LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
@@ -976,7 +980,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         is->bsdf = (int)RRT_ZERO_BSDF;  // a hit whose radiance is +0: no record, no shading
         return true;
       }
-      return query_nx<false, false, RRT_BATCH_CALL, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, is, cn);
+      return query_nx<false, false, RRT_BCALL(LEAN), LEAN == V_KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, is, cn);
     };
     const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;  // this group's lanes
     const uint64_t lt = ((1ull << lane) - 1ull) & gmask;                         // group lanes before me
@@ -1112,9 +1116,9 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN, RRT_BATCH_CALL>(kp, g, cl, t, cn);
-      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
+      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BCALL(LEAN), RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN, RRT_BCALL(LEAN)>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, RRT_BCALL(LEAN), RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
     }
     if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
