@@ -1232,6 +1232,21 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 // samples_per_batch) and count * draws_miss draws -- written here.  The others go to the claim
 // list, appended per wave (one atomic) so claims keep their order within each wave's run.
 // Claim index ix of the pass (a whole wave calls it together: ballots and one atomic per wave).
+#ifndef RRT_HEAVY_STRADDLE
+#define RRT_HEAVY_STRADDLE 0  // 1: listed pixels with a proven-miss corner ray go to the heavy list too (A/B)
+#endif
+// A listed pixel (not every ray a proven miss) one of whose corner rays is a proven miss straddles
+// the scene's silhouette: its samples mix hits and misses, the costliest case of the batch kernel's
+// slot speculation (several rounds per step).  A routing heuristic only, like pixel_heavy.
+__device__ __forceinline__ bool pixel_straddles(const KParams& kp, uint32_t x, uint32_t y) {
+  using namespace rrt;
+  Counters cn = {};
+  bool any = false;
+#pragma unroll 1
+  for (int k = 0; k < 4 && !any; ++k)
+    any = camera_miss_proof<false>(kp, ld3(kp.cam.pos), pixel_ray_dir(kp, (double)x + (k & 1), (double)y + (k >> 1)), cn);
+  return any;
+}
 __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, uint32_t lane) {
   using namespace rrt;
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
@@ -1247,7 +1262,7 @@ __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, u
         if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
       } else {
         listed = true;
-        heavy = kp.heavy_list && pixel_heavy(kp, x, y);
+        heavy = kp.heavy_list && (pixel_heavy(kp, x, y) || (RRT_HEAVY_STRADDLE && pixel_straddles(kp, x, y)));
       }
     }
   }
