@@ -333,14 +333,13 @@ int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 int rrt_libm_eval(rrt_ctx* ctx, int fn, const double* a, const double* b, double* out, uint64_t n);
 /* Run-time proof audit.  The renderer skips marches whose results its proofs
  * determine (camera-ray miss, shadow-ray occlusion, pixel and strip miss, Kerr occlusion); their
- * margins are validated by sweeps; the camera-ray hit proof with the occlusion proofs turns samples into
- * +0 without their exact march (zero samples).  With the audit set, every counting launch that runs the proofs
+ * margins are validated by sweeps.  With the audit set, every counting launch that runs the proofs
  * (RRT_RENDER_COUNTERS | RRT_RENDER_COUNT_EXECUTED) also marches every 2^every_log2-th proven ray
  * (every 2^every_log2-th pixel for the pixel pass) exactly and tallies disagreements.  Render
  * outputs are unchanged.  rrt_get_proof_audit (synchronises the device) returns and resets the
  * tallies: out[2 k] rays checked, out[2 k + 1] violations, k = RRT_AUDIT_CAMERA .. RRT_AUDIT_ZERO. */
 enum { RRT_AUDIT_CAMERA = 0, RRT_AUDIT_SHADOW = 1, RRT_AUDIT_PIXEL = 2, RRT_AUDIT_STRIP = 3, RRT_AUDIT_KERR = 4,
-       RRT_AUDIT_ZERO = 5 /* zero samples: camera hit proof + occlusion proofs -> radiance +0 */,
+       RRT_AUDIT_ZERO = 5 /* reserved: the zero-sample variant (round 5) was removed; always 0 */,
        RRT_AUDIT_KINDS = 6 };
 int rrt_set_proof_audit(rrt_ctx* ctx, int every_log2 /* < 0: off (the default) */);
 int rrt_get_proof_audit(rrt_ctx* ctx, uint64_t* out /* [2 * RRT_AUDIT_KINDS] */);

@@ -42,10 +42,7 @@ __device__ __forceinline__ v3 cross(v3 u, v3 v) {
 // checks) around a core of v_rsq / v_rcp + FMA refinements.  For operands of magnitude in
 // [2^-300, 2^300] the scaling is never triggered and the fix-ups are identities, so the bare
 // core below returns the same bits (checked bit for bit by tests/test_gpu_parity.py); other
-// operands take the library path.  RRT_LIBM_DIVSQRT=1 builds without the fast path (A/B).
-#ifndef RRT_LIBM_DIVSQRT
-#define RRT_LIBM_DIVSQRT 0
-#endif
+// operands take the library path.
 __device__ __forceinline__ bool in_core_range(double v) {
   const double a = fabs(v);
   return a >= 0x1p-300 && a <= 0x1p300;
@@ -72,11 +69,11 @@ __device__ __forceinline__ double div_core(double a, double b) {  // = llvm f64 
   return fma(r, y, q);
 }
 __device__ __forceinline__ double xsqrt(double x) {
-  if (RRT_LIBM_DIVSQRT || __builtin_expect(!in_core_range(x), 0)) return sqrt(x);
+  if (__builtin_expect(!in_core_range(x), 0)) return sqrt(x);
   return sqrt_core(x);
 }
 __device__ __forceinline__ double xdiv(double a, double b) {
-  if (RRT_LIBM_DIVSQRT || __builtin_expect(!(in_core_range(a) && in_core_range(b)), 0)) return a / b;
+  if (__builtin_expect(!(in_core_range(a) && in_core_range(b)), 0)) return a / b;
   return div_core(a, b);
 }
 __device__ __forceinline__ double norm(v3 a) { return xsqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
@@ -164,9 +161,6 @@ __device__ __forceinline__ bool in_fast_range(double v) {
   const double a = fabs(v);
   return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p20);
 }
-#ifndef RRT_SLAB_APPROX
-#define RRT_SLAB_APPROX 1  // 0: every fast slab test takes the Markstein quotients (A/B)
-#endif
 // BBox::intersect (bbox.cpp:10-25), dividing by the segment direction; min_t is 0 for every
 // micro segment.  EXACT: IEEE division; else qdiv with the per-segment reciprocals y.
 template <bool EXACT>
@@ -179,7 +173,6 @@ __device__ __forceinline__ bool slab(const double* mn, const double* mx, v3 o, v
   } else {
     const double nx0 = mn[0] - o.x, nx1 = mx[0] - o.x, ny0 = mn[1] - o.y, ny1 = mx[1] - o.y,
                  nz0 = mn[2] - o.z, nz1 = mx[2] - o.z;
-#if RRT_SLAB_APPROX
     {  // approximate-then-verify: the products n * y are within 2^-50 (relative to the result of
        // the min / max chains) of the exact RN(n / d) on a fast segment, so a decision that
        // holds with a 2^-45 relative margin is the exact test's decision; the rest go exact.
@@ -192,7 +185,6 @@ __device__ __forceinline__ bool slab(const double* mn, const double* mx, v3 o, v
       if (amin > amax + m1 || amin > max_t + m2 || amax < -m3) return false;
       if (amin <= amax - m1 && amin <= max_t - m2 && amax >= m3) return true;
     }
-#endif
     tx0 = qdiv(nx0, d.x, y.x); tx1 = qdiv(nx1, d.x, y.x);
     ty0 = qdiv(ny0, d.y, y.y); ty1 = qdiv(ny1, d.y, y.y);
     tz0 = qdiv(nz0, d.z, y.z); tz1 = qdiv(nz1, d.z, y.z);
@@ -719,10 +711,6 @@ __device__ __forceinline__ void next_micro_impl(const DHole& h, v3 no, v3& o, v3
 __device__ __forceinline__ void next_micro_at(const DHole& h, v3 no, v3& o, v3& d, double& max_t, v3& rel,
                                               double& rel2, MicroOut* mo = nullptr) {
   bool ok = true;
-  if (RRT_LIBM_DIVSQRT) {
-    next_micro_impl<false>(h, no, o, d, max_t, rel, rel2, ok, mo);
-    return;
-  }
   const v3 d0 = d;
   next_micro_impl<true>(h, no, o, d, max_t, rel, rel2, ok, mo);
   if (__builtin_expect(!ok, 0)) {  // some operand outside the core's range: the IEEE step
@@ -977,22 +965,15 @@ __device__ __forceinline__ bool audit_pick(const KParams& kp, v3 o, v3 d) {
   return (h & ((1ull << kp.audit_shift) - 1ull)) == 0ull;
 }
 __device__ __forceinline__ void audit_note(const KParams& kp, int k, bool violated) {
-  atomicAdd(kp.audit + 2 * k, 1u);
-  if (violated) atomicAdd(kp.audit + 2 * k + 1, 1u);
+  atomicAdd(kp.audit + 2 * k, 1ull);
+  if (violated) atomicAdd(kp.audit + 2 * k + 1, 1ull);
 }
 __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 d);
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn);
-template <bool COUNT>
-__device__ __forceinline__ bool kerr_shadow(const KParams& kp, v3 o, v3 d, Counters& cn);
-#ifndef RRT_KERR_SHADOW_LOOP
-#define RRT_KERR_SHADOW_LOOP 0  // 1: the proof's coarse march and the exact march in one loop (A/B, kerr_shadow)
-#endif
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool query_kerr(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   // shadow rays: the occlusion proof first (never in the reference-work counts)
-  if (RRT_KERR_SHADOW_LOOP && !RRT_LIBM_DIVSQRT && ANY && kp.kproof.on && !(COUNT && !kp.count_exec))
-    return kerr_shadow<COUNT>(kp, o, d, cn);
   if (ANY && kp.kproof.on && !(COUNT && !kp.count_exec) && kerr_occluded_proof(kp, o, d)) {
     if (COUNT && kp.audit && audit_pick(kp, o, d)) {
       Counters c2 = {};
@@ -1014,7 +995,7 @@ __device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect*
   for (int j = 0; j < h.kerr_max_steps && swept < 2.0 * PI_D; ++j) {
     v3 q1 = q, p1 = p;
     double sw1 = swept;
-    KArith<!RRT_LIBM_DIVSQRT> fast;
+    KArith<true> fast;
     bool escaped = kerr_advance(h, q1, p1, sw1, fast);
     if (__builtin_expect(!fast.ok, 0)) {  // an operand outside the cores' range: the IEEE step
       KArith<false> ieee;
@@ -1037,9 +1018,6 @@ __device__ __forceinline__ bool kerr_march(const KParams& kp, v3 o, v3 d, Isect*
 }
 
 // ------------------------------------------------------------------ shadow-ray occlusion proof
-#ifndef RRT_SHADOW_PROOF
-#define RRT_SHADOW_PROOF 1  // 0: build without the occlusion proof (A/B)
-#endif
 // (DESIGN.md §5).  The reference's shadow query (bvh.cpp:103-113; the caller uses only the
 // boolean) is true iff some micro segment before the capture hits a primitive.  Most shadow rays
 // of a closed room end on a wall, after ~15-30 exact steps and walks.  The proof marches the
@@ -1087,9 +1065,8 @@ __device__ __forceinline__ int occ_exit(const KParams& kp, v3 a, v3 b, double m)
   }
   return out ? -1 : 0;
 }
-#ifndef RRT_SHADOW_MODE
-#define RRT_SHADOW_MODE 2  // A/B: 0 inline; 1 the whole proof out of line; 2 occ_exit out of line
-#endif
+// occ_exit out of line, one copy per kernel build W (inline or the whole proof out of
+// line measured slower)
 template <int W>
 __device__ __noinline__ int occ_exit_call(const KParams& kp, v3 a, v3 b, double m) { return occ_exit(kp, a, b, m); }
 __device__ __forceinline__ bool occ_inside(const DShadowProof& sp, v3 b) {
@@ -1196,105 +1173,11 @@ __device__ __forceinline__ bool kerr_occluded_proof(const KParams& kp, v3 o, v3 
   }
   return false;
 }
-// Kerr shadow query in one loop (query_kerr with the proof on): the occlusion proof's coarse march
-// and, when it gives no proof, the exact march from the start, as one sequence of RK4 steps per
-// lane.  Run as two loops, a wave spends the longest coarse march of its lanes and then their
-// longest exact march; here a lane leaving the proof starts its exact march at the next step, so
-// the wave runs the longest coarse + exact sequence of any one lane, and lanes in either mode share
-// the step's four Hamiltonian evaluations.  Each mode's steps, tests and results are those of
-// kerr_occluded_proof and kerr_march (the exact step's stretch is 1: (dt r) * 1 is dt r exactly).
-template <bool COUNT>
-__device__ __forceinline__ bool kerr_shadow(const KParams& kp, v3 o, v3 d, Counters& cn) {
-  const DHole& h = kp.hole;
-  const DKerrProof& kq = kp.kproof;
-  const double rh2 = h.r_hor * h.r_hor;
-  const v3 c = ld3(h.c);
-  v3 q, p;
-  kerr_init(h, o, d, q, p);
-  bool coarse = kerr_proof_worth(kp, o, d) && norm2(q) > kq.r_near2;
-  v3 a = o, a0 = o;  // the chord's (segment's) start; the proof's previous chord start
-  bool a_in = occ_inside(kp.occ, a);
-  double swept = 0.0;
-  int j = 0;
-  bool restart = false;  // the proof gave up: the exact march starts from the ray at the next step
-#pragma unroll 1
-  for (;;) {
-    if (restart) {
-      restart = false;
-      coarse = false;
-      kerr_init(h, o, d, q, p);
-      a = o; swept = 0.0; j = 0;
-    }
-    if (coarse ? !(j < kq.max_steps) : !(j < h.kerr_max_steps && swept < 2.0 * PI_D)) {
-      if (!coarse) return false;
-      restart = true;
-      continue;
-    }
-    v3 q1 = q, p1 = p;
-    double sw1 = swept;
-    KArith<true> fast;
-    bool escaped = kerr_advance(h, q1, p1, sw1, fast, coarse ? kq.stretch : 1.0);
-    if (__builtin_expect(!fast.ok, 0)) {
-      if (coarse) { restart = true; continue; }
-      KArith<false> ieee;  // the exact march's step with an operand outside the cores' range
-      q1 = q; p1 = p; sw1 = swept;
-      escaped = kerr_advance(h, q1, p1, sw1, ieee);
-    }
-    if (coarse) {  // kerr_occluded_proof's step
-      if (escaped || !(sw1 < kq.swept_max) || !(norm2(q1) > kq.r_near2)) { restart = true; continue; }
-      q = q1; p = p1; swept = sw1;
-      const v3 b = kerr_world(h, q);
-      {
-        const v3 u = b - a, w = c - a;
-        const double uu = norm2(u), t = uu > 0.0 ? fmin(fmax(dot(u, w) / uu, 0.0), 1.0) : 0.0;
-        if (!(norm2(w - vmul(u, t)) > kq.r_near2)) { restart = true; continue; }
-      }
-      const bool b_in = occ_inside(kp.occ, b);
-      if (!b_in || !a_in) {
-        int res = occ_exit_quad(kp, a, b, kq.delta);
-        if (res <= 0 && j > 0) {
-          const v3 u = b - a0, w = a - a0;
-          const double uu = norm2(u), uw = dot(u, w);
-          const double beta = sqrt(fmax(norm2(w) - uw * uw / uu, 0.0)) * (1.0 + 1e-6);
-          if (uu > 0.0 && occ_exit_quad(kp, a0, b, kq.delta + beta) > 0) res = 1;
-        }
-        if (res > 0) {
-          if (COUNT && kp.audit && audit_pick(kp, o, d)) {
-            Counters c2 = {};
-            audit_note(kp, RRT_AUDIT_KERR, !kerr_march<true, false>(kp, o, d, nullptr, c2));
-          }
-          return true;
-        }
-        if (res < 0) { restart = true; continue; }
-      }
-      a_in = b_in;
-      a0 = a;
-      a = b;
-      ++j;
-      continue;
-    }
-    // kerr_march's step
-    if (escaped) return false;
-    q = q1; p = p1; swept = sw1;
-    if (COUNT) cn.micro++;
-    if (kerr_r2(h, q) <= rh2) return false;  // captured
-    const v3 b = kerr_world(h, q);
-    const v3 seg = b - a;
-    const double max_t = norm(seg);
-    const double inv = xdiv(1., max_t);
-    const v3 sd = V(seg.x * inv, seg.y * inv, seg.z * inv);
-    if (segment_query<true, COUNT, false>(kp, a, sd, max_t, a + vmul(sd, max_t), nullptr, cn)) return true;
-    a = b;
-    ++j;
-  }
-}
 // The whole march by the recurrence, step 0 included: the ray (o, d) is the state of a step from
 // the point A = o itself (|A - c| = 1 / u, so v_prev = rho u, E_prev = x, s_prev chosen so the
 // update yields s = u and the reference's u' = -u (d . x) / |d - (d . x) x|).
-// ms: margin scale (1; the zero-sample proof, whose ray starts at the camera hit proof's crossing
-// point rather than at the reference's hit point, takes RRT_ZERO_MS)
 template <int W = 0>
-__device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v3 d, int steps, double ms = 1.0) {
+__device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v3 d, int steps) {
 #pragma clang fp contract(fast)
   const DMissProof& mp = kp.miss;
   const DShadowProof& sp = kp.occ;
@@ -1329,7 +1212,7 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
     sig *= sg;
     const double av = fabs(v), avp = fabs(vprev);
     const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);  // |B - c| (upper bound)
-    const double m = (ms * mp.eta) * (fmax(rp, r) + mp.scale);
+    const double m = mp.eta * (fmax(rp, r) + mp.scale);
     // the segment must clear the capture sphere: its distance from the hole > r_s + m (the
     // camera proof's scalar distance: foot of the perpendicular inside, else the nearer end)
     const double rb = rc + m;
@@ -1345,138 +1228,10 @@ __device__ __forceinline__ bool shadow_occluded_proof(const KParams& kp, v3 o, v
       const double ia = mp.rho / vprev;
       const v3 pa = V(c.x + (ea * ia) * X.x + (eb * ia) * Y.x, c.y + (ea * ia) * X.y + (eb * ia) * Y.y,
                       c.z + (ea * ia) * X.z + (eb * ia) * Y.z);
-      const int res = RRT_SHADOW_MODE == 2 ? occ_exit_call<W>(kp, pa, pb, m) : occ_exit(kp, pa, pb, m);
+      const int res = occ_exit_call<W>(kp, pa, pb, m);
       if (res) return res > 0;
     }
     a_in = b_in;
-    rp = r; vprev = v; ea = na; eb = nb;
-  }
-  return false;
-}
-
-// ------------------------------------------------------------------ camera-ray hit proof
-// ("zero samples").  91% of the cfg3 camera rays that reach the room first hit one of
-// the room's face triangles (walls, floor, ceiling: the occlusion proof's table), and from there
-// nearly every light sample's shadow ray is occluded, so the sample's radiance is +0 -- yet each such
-// sample marched its camera ray exactly (~12 micro steps and walks).  The proof marches the shadow
-// proof's recurrence from the camera ray itself and accepts "the reference's query hits kept face
-// triangle T, not a light, at a point within the recurrence's deviation of Q" when, at the shadow
-// proof's margin m for every segment up to the crossing:
-//   * the segment clears the capture sphere (a capture would end the query first, with no hit);
-//   * it clears the box holding every primitive but the kept face triangles (kp.occ.nocc_*);
-//   * every kept triangle of a face an end of it is past is certainly untouched (ends more than m on
-//     one side of its plane, or its plane crossing mq outside an edge) -- but one, T, which the
-//     segment certainly crosses (ends more than m on either side, the crossing point mq inside
-//     every edge).  Triangles of faces no end is past lie beyond the trigger box: untouched.
-// The reference's segments are within the recurrence's deviation (a small fraction of m) of these,
-// so its query reaches T's segment uncaptured, no primitive before it is hit, and T's test accepts:
-// its hit is T, at a point within that deviation of Q.  Anything else -- an uncertain triangle, two
-// crossings in one segment, a light, the ray leaving the room -- is no proof.
-// occ_touch: 2 = certain crossing (at q), 0 = certainly untouched, 1 = uncertain (NaN: 1)
-__device__ __forceinline__ int occ_touch(const DOccluder& t, v3 a, v3 b, double m, v3& q) {
-#pragma clang fp contract(fast)
-  const double da = t.n[0] * a.x + t.n[1] * a.y + t.n[2] * a.z - t.d;
-  const double db = t.n[0] * b.x + t.n[1] * b.y + t.n[2] * b.z - t.d;
-  if ((da > m && db > m) || (da < -m && db < -m)) return 0;
-  if (!((da > m && db < -m) || (da < -m && db > m))) return 1;
-  const double tq = da / (da - db);
-  q = V(a.x + (b.x - a.x) * tq, a.y + (b.y - a.y) * tq, a.z + (b.z - a.z) * tq);
-  const double mq = m * (2.0 + (fabs(b.x - a.x) + fabs(b.y - a.y) + fabs(b.z - a.z)) / fabs(da - db));
-  bool in = true, out = false;
-  for (int k = 0; k < 3; ++k) {
-    const double e = t.en[k][0] * q.x + t.en[k][1] * q.y + t.en[k][2] * q.z - t.eo[k];
-    in = in && e >= mq;
-    out = out || e <= -mq;
-  }
-  return in ? 2 : out ? 0 : 1;
-}
-// The kept triangles a segment with an end outside the trigger box may touch: -1 = no proof (an
-// uncertain one, or two crossings), else the number of certain crossings (0 or 1: face f, index i, q)
-__device__ __noinline__ int occ_first_cross(const KParams& kp, v3 a, v3 b, double m, int& fi, v3& q) {
-  const DShadowProof& sp = kp.occ;
-  int found = 0;
-#pragma unroll 1
-  for (int f = 0; f < 6; ++f) {
-    const int k = f < 3 ? f : f - 3;
-    const double ak = k == 0 ? a.x : k == 1 ? a.y : a.z, bk = k == 0 ? b.x : k == 1 ? b.y : b.z;
-    const bool past = f < 3 ? !(bk >= sp.in_lo[k] && ak >= sp.in_lo[k]) : !(bk <= sp.in_hi[k] && ak <= sp.in_hi[k]);
-    if (!past) continue;
-#pragma unroll 1
-    for (uint32_t i = 0; i < sp.n[f]; ++i) {
-      v3 qq;
-      const int r = occ_touch(sp.tri[f][i], a, b, m, qq);
-      if (r == 1 || (r == 2 && found)) return -1;
-      if (r == 2) { found = 1; fi = 4 * f + (int)i; q = qq; }
-    }
-  }
-  return found;
-}
-__device__ __forceinline__ bool in_box(const double* lo, const double* hi, v3 p) {
-  return p.x >= lo[0] && p.x <= hi[0] && p.y >= lo[1] && p.y <= hi[1] && p.z >= lo[2] && p.z <= hi[2];
-}
-__device__ __forceinline__ bool seg_clear_of_box(v3 a, v3 b, const double* lo, const double* hi, double m);
-__device__ __forceinline__ bool camera_hit_proof(const KParams& kp, v3 o, v3 d, v3& Q) {
-#pragma clang fp contract(fast)
-  const DMissProof& mp = kp.miss;
-  const DShadowProof& sp = kp.occ;
-  const DHole& h = kp.hole;
-  const v3 c = V(h.c[0], h.c[1], h.c[2]);
-  const v3 x0 = o - c;
-  const double r0 = sqrt(norm2(x0)), u0 = 1.0 / r0;
-  const v3 X = vmul(x0, u0);
-  const double dx = dot(d, X);
-  v3 Y = d - smul(dx, X);
-  const double dy = sqrt(norm2(Y));
-  if (!(dy > 1e-3)) return false;  // towards the hole
-  Y = vmul(Y, 1.0 / dy);
-  const double up0 = -u0 * dx / dy;
-  double vprev = mp.rho * u0, s = u0 * mp.co1 - up0 * h.sin_dt * mp.inv_rho;
-  double ea = 1.0, eb = 0.0, sig = 1.0, rp = r0;
-  bool a_in = occ_inside(sp, o), a_room = in_box(mp.lo, mp.hi, o);
-  v3 pa = o;
-  const double si2 = h.sin_dt * h.sin_dt, rc = h.r * (1.0 + 1e-9);
-#pragma unroll 1
-  for (int j = 0; j < h.steps; ++j) {
-    const double sg = vprev < 0.0 ? -1.0 : 1.0;
-    const double up = (vprev * mp.co1 - mp.rho * s) * mp.inv_si;
-    s = fabs(vprev) * mp.inv_rho;
-    const double f1 = -s + mp.k15 * s * s;
-    const double u2 = s + up * (h.dt * 0.5);
-    const double f2 = -u2 + mp.k15 * u2 * u2;
-    const double u3 = u2 + f1 * mp.dt2_4;
-    const double f3 = -u3 + mp.k15 * u3 * u3;
-    const double v = s + up * h.dt + (f1 + f2 + f3) * mp.dt2_6;
-    if (!(fabs(v) >= mp.kappa * (s + fabs(up) * h.dt))) return false;  // cancelling step (or NaN)
-    const double a = sg * mp.co1, b = sig * mp.si1;
-    const double na = a * ea - b * eb, nb = a * eb + b * ea;
-    sig *= sg;
-    const double av = fabs(v), avp = fabs(vprev);
-    const double r = mp.rho * __builtin_amdgcn_rcp(av) * (1.0 + 1e-6);
-    const double m = mp.eta * (fmax(rp, r) + mp.scale);
-    const double rb = rc + m;  // clear of the capture sphere
-    const double D = v * v + vprev * vprev - 2.0 * mp.co1 * avp * v;
-    const bool inside = v * (mp.co1 * avp - v) < 0.0 && avp * (avp - mp.co1 * v) > 0.0;
-    const bool clear = inside ? si2 > rb * rb * D : mp.rho * mp.rho > rb * rb * fmax(v * v, vprev * vprev);
-    if (!clear) return false;
-    const double ib = mp.rho / v;
-    const v3 pb = V(c.x + (na * ib) * X.x + (nb * ib) * Y.x, c.y + (na * ib) * X.y + (nb * ib) * Y.y,
-                    c.z + (na * ib) * X.z + (nb * ib) * Y.z);
-    const bool b_in = occ_inside(sp, pb);
-    int fi = -1, found = 0;
-    v3 q = pb;
-    if (!(a_in && b_in)) {
-      found = occ_first_cross(kp, pa, pb, m, fi, q);
-      if (found < 0) return false;
-    }
-    if (!seg_clear_of_box(pa, pb, sp.nocc_lo, sp.nocc_hi, m)) return false;  // clear of every other primitive
-    if (found) {
-      if ((sp.emit[fi >> 2] >> (fi & 3)) & 1u) return false;  // a light: its hit is not black
-      Q = q;
-      return true;
-    }
-    const bool b_room = in_box(mp.lo, mp.hi, pb);
-    if (a_room && !b_room) return false;  // leaving the room without a crossing
-    a_in = b_in; a_room = b_room; pa = pb;
     rp = r; vprev = v; ea = na; eb = nb;
   }
   return false;
@@ -1490,9 +1245,6 @@ __device__ __forceinline__ bool camera_hit_proof(const KParams& kp, v3 o, v3 d, 
 #define RRT_QACC(v) do { if (ANY) cn.t_squery += clock64() - v; else cn.t_query += clock64() - v; } while (0)
 #else
 #define RRT_QACC(v)
-#endif
-#ifndef RRT_QUERY_AHEAD
-#define RRT_QUERY_AHEAD 0  // 1: lanes skip ahead to their next walk (A/B; slower, profiles/r04_ab_query_ahead.txt)
 #endif
 #ifndef RRT_QUERY_ATTR  // inline into every kernel build: a query shared out of line by builds of
                         // different waves-per-SIMD budgets takes the loosest budget's registers, and
@@ -1510,43 +1262,6 @@ RRT_QUERY_ATTR bool query(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn
   RRT_T0(tq0);
   double max_t = 0.0;
   v3 e = o + vmul(d, max_t);  // the next segment's start (micro = Ray(o, d, max_t = 0), bvh.cpp:104)
-#if RRT_QUERY_AHEAD
-  // Lanes meet at walks, not at step indices: each lane advances its own march to its next
-  // segment that needs a walk (not captured, not skipped), then the wave's lanes walk together.
-  // Stepping in lock-step by index would make every lane wait, at each step, for the longest
-  // walk any lane has at that index.  Same steps and walks per lane, in the same order.
-  if (!COUNT) {
-    int j = 0;
-#pragma unroll 1
-    for (;;) {
-      bool walk = false;
-      int cell = -1;
-#pragma unroll 1
-      while (j < kp.hole.steps) {
-        RRT_T0(tm0);
-        v3 rel;
-        double rel2;
-        next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
-        RRT_ACC(t_micro, tm0);
-        ++j;
-        if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) break;  // captured: no hit
-        e = o + vmul(d, max_t);
-        if (segment_outside_root(kp, o, e)) continue;
-        cell = grid_cell(kp.grid, o);
-        if (cell_clear(kp.grid, cell, max_t)) continue;
-        walk = true;
-        break;
-      }
-      if (!walk) break;
-      if (segment_walk<ANY, false, W4>(kp, o, d, max_t, e, cell, is, cn, any_rt)) {
-        RRT_QACC(tq0);
-        return true;
-      }
-    }
-    RRT_QACC(tq0);
-    return false;
-  }
-#endif
   for (int j = 0; j < kp.hole.steps; ++j) {
     RRT_T0(tm0);
     v3 rel;
@@ -1878,31 +1593,18 @@ __device__ __forceinline__ bool pixel_heavy(const KParams& kp, uint32_t px, uint
   return cap[0] != cap[1] || (close && !(cap[0] && cap[1]));
 }
 
-// query() behind a call: the caller keeps only what is live across the call, the walk gets the
-// register file to itself (rrt_sample.hip batch kernel)
-template <bool ANY, bool KERR, bool W4 = true>
-__device__ __noinline__ bool query_call(const KParams& kp, v3 o, v3 d, Isect* is) {
-  Counters cn = {};
-  return query<ANY, false, KERR, W4>(kp, o, d, is, cn);
-}
-// The occlusion proof's build tag W (0: no proof in this build).  Its out-of-line parts (the
-// face test, or the whole proof in mode 1) get one copy per calling kernel build: a callee shared
-// by kernels of different waves-per-SIMD budgets gets the smallest budget's registers, and every
-// caller then allocates the callee's count.  Measured on cfg3 (profiles/r02_ab_log.md): inline
-// 31.5 ms, face test out of line 31.3, whole proof out of line 37.6 (the call's frame and SGPR
-// saves), no proof 35.3.
-template <int W>
-__device__ __noinline__ bool shadow_proof_call(const KParams& kp, v3 o, v3 d) {
-  return shadow_occluded_proof(kp, o, d, kp.hole.steps);
-}
-// W: the occlusion proof's build tag (0: none)
-template <bool ANY, bool COUNT, bool NI, bool KERR = false, int W = 0, bool W4 = true>
+// W: the occlusion proof's build tag (0: no proof in this build).  Its out-of-line part (the face
+// test, occ_exit_call) gets one copy per calling kernel build: a callee shared by kernels of
+// different waves-per-SIMD budgets gets the smallest budget's registers, and every caller then
+// allocates the callee's count.  Measured on cfg3 (profiles/r02_ab_log.md): inline 31.5 ms, face
+// test out of line 31.3, whole proof out of line 37.6 (the call's frame and SGPR saves), no proof
+// 35.3.
+template <bool ANY, bool COUNT, bool KERR = false, int W = 0, bool W4 = true>
 __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* is, Counters& cn) {
   // shadow rays: the occlusion proof first (Schwarzschild; never in the reference-work counts)
-  if (RRT_SHADOW_PROOF && W && ANY && !KERR && kp.occ.on && !(COUNT && !kp.count_exec)) {
+  if (W && ANY && !KERR && kp.occ.on && !(COUNT && !kp.count_exec)) {
     RRT_T0(tp0);
-    const bool occluded = RRT_SHADOW_MODE == 1 ? shadow_proof_call<W>(kp, o, d)
-                                               : shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
+    const bool occluded = shadow_occluded_proof<W>(kp, o, d, kp.hole.steps);
     RRT_ACC(t_squery, tp0);
     if (occluded) {
       if (COUNT && kp.audit && audit_pick(kp, o, d)) {
@@ -1912,7 +1614,6 @@ __device__ __forceinline__ bool query_nx(const KParams& kp, v3 o, v3 d, Isect* i
       return true;
     }
   }
-  if (NI && !COUNT) return query_call<ANY, KERR, W4>(kp, o, d, is);
   return query<ANY, COUNT, KERR, W4>(kp, o, d, is, cn);
 }
 

@@ -33,11 +33,6 @@ hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, 
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, bool strips, hipStream_t stream);
-// The pixel pass's first level (rrt_sample.hip rrt_strip_proof_kernel): strips of 64 claim indices
-// proven as wholes before the per-pixel level; 0 for the per-pixel pass alone (A/B)
-#ifndef RRT_STRIP_PASS
-#define RRT_STRIP_PASS 1
-#endif
 hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_path(const KParams* d_kp, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
@@ -128,7 +123,7 @@ struct rrt_ctx {
   // heavy pixels (rrt_pixel_proof_kernel's heavy list, taken first by the batch kernel's waves)
   uint32_t* d_heavy_list = nullptr;
   uint32_t* d_strip_list = nullptr;  // the pixel pass's strips left to the per-pixel level
-  uint32_t* d_audit = nullptr;       // proof-audit tallies (rrt_set_proof_audit), 16 words
+  unsigned long long* d_audit = nullptr;  // proof-audit tallies (rrt_set_proof_audit), 16 64-bit words
   uint32_t audit_shift = 0;          // 0: no audit; else re-check every 2^(audit_shift - 1)-th proven ray
   size_t strip_list_cap = 0;
   size_t heavy_list_cap = 0;
@@ -510,7 +505,6 @@ static void build_occluders(rrt_ctx* c) {
       if (ok) cand[f].push_back({0.5 * nl, w, t, {q[0], q[1], q[2]}, pi});
     }
   }
-  std::vector<uint8_t> kept(c->prims.size(), 0);
   for (int f = 0; f < 6; ++f) {
     std::stable_sort(cand[f].begin(), cand[f].end(), [](const Cand& x, const Cand& y) { return x.area > y.area; });
     size_t keep = std::min<size_t>(cand[f].size(), RRT_OCC_PER_FACE);
@@ -519,9 +513,6 @@ static void build_occluders(rrt_ctx* c) {
     for (uint32_t i = 0; i < o.n[f]; ++i) {
       o.tri[f][i] = cand[f][i].t;
       o.w[f] = std::max(o.w[f], cand[f][i].w);
-      const uint32_t b = c->prims[cand[f][i].prim].bsdf;
-      if (b >= c->bsdfs.size() || c->bsdfs[b].type == RRT_BSDF_EMISSION) o.emit[f] |= 1u << i;  // a light
-      kept[cand[f][i].prim] = 1;
     }
     // The Kerr proof's wall pieces: two kept triangles that share an edge (vertices within 1e-9 of
     // the box's extent), lie in one plane and form a convex quad are one piece -- the crossing may
@@ -576,13 +567,6 @@ static void build_occluders(rrt_ctx* c) {
     }
     c->occ_nq[f] = nq;
   }
-  // The camera-ray hit proof (rrt_device.h camera_hit_proof): every primitive but the kept face
-  // triangles lies in this box (empty: lo > hi); a segment that clears it touches no such primitive
-  Box nb = Box::empty();
-  for (uint32_t pi = 0; pi < (uint32_t)c->prims.size(); ++pi)
-    if (!kept[pi]) nb.expand(prim_box(c, c->prims[pi]));
-  o.nocc_lo[0] = nb.mn.x; o.nocc_lo[1] = nb.mn.y; o.nocc_lo[2] = nb.mn.z;
-  o.nocc_hi[0] = nb.mx.x; o.nocc_hi[1] = nb.mx.y; o.nocc_hi[2] = nb.mx.z;
 }
 
 static void build_free_grid(rrt_ctx* c) {
@@ -1467,12 +1451,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     // the point-light scenes' builds carry no proof (rrt_sample.hip RRT_OCC_TAG); off for them in
     // every kernel, so the counting passes count what their batch kernel executes
     kp.occ.on = (proofs_valid && any && fin && c->lean != 2 && !(p->flags & RRT_RENDER_NO_SHADOW_PROOF)) ? 1u : 0u;
-    // zero samples (rrt_sample.hip zero_sample_proof): the camera-ray hit proof plus the occlusion
-    // proof, for the area-light scenes (A/B and parity: RRT_AB_NO_ZERO=1 in the environment)
-    {
-      const char* nz = std::getenv("RRT_AB_NO_ZERO");
-      kp.occ.hit_on = (kp.occ.on && c->lean == 1 && !(nz && nz[0] == '1') && !(p->flags & RRT_RENDER_NO_MISS_PROOF)) ? 1u : 0u;
-    }
     // Kerr shadow rays (rrt_device.h kerr_occluded_proof): the same face triangles
     // against a coarse march, inside the envelope its margin was swept over
     // (tools/kerr_proof_sweep.py -> profiles/r04_kerr_proof_sweep.json)
@@ -1757,7 +1735,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
   }
   // the pass's strip level: tiles whose rows split into strips of 64 claim indices (ts | 64 or 64 | ts)
-  if (kp.claim_list && RRT_STRIP_PASS && (RRT_CLAIM_BLOCK8 || 64u % ts == 0u || ts % 64u == 0u) && kp.n_pixels >= 64u) {
+  if (kp.claim_list && kp.n_pixels >= 64u) {
     const size_t ns = kp.n_pixels / 64u;
     if (c->strip_list_cap < ns) {
       hipFree(c->d_strip_list); c->d_strip_list = nullptr;
@@ -1821,11 +1799,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // tail priority threshold (A/B: RRT_AB_PRIO_TICKS in the environment)
   kp.prio_ticks = 50000u;
   if (const char* pt = std::getenv("RRT_AB_PRIO_TICKS")) kp.prio_ticks = (uint32_t)std::strtoul(pt, nullptr, 10);
-  // dealt shadow walks in the batch kernel's LEAN builds (A/B and parity: RRT_AB_NO_DEAL=1 in the environment)
-  {
-    const char* nd = std::getenv("RRT_AB_NO_DEAL");
-    kp.deal = (nd && nd[0] == '1') ? 0u : 1u;
-  }
   HIPCHK(c, hipMemcpyAsync(c->d_kp, &kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   const uint32_t ring = (uint32_t)(c->n_launch % rrt_ctx::kRing);
   HIPCHK(c, hipEventRecord(c->ev0[ring], stream));
@@ -2102,8 +2075,8 @@ extern "C" int rrt_set_proof_audit(rrt_ctx* c, int every_log2) {
   if (c->device < 0) return fail(c, RRT_E_NO_DEVICE, "host-only context cannot render");
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->d_audit) {
-    HIPCHK(c, hipMalloc(&c->d_audit, sizeof(uint32_t) * 16));
-    HIPCHK(c, hipMemset(c->d_audit, 0, sizeof(uint32_t) * 16));
+    HIPCHK(c, hipMalloc(&c->d_audit, sizeof(unsigned long long) * 16));
+    HIPCHK(c, hipMemset(c->d_audit, 0, sizeof(unsigned long long) * 16));
   }
   c->audit_shift = (uint32_t)every_log2 + 1u;
   return RRT_OK;
@@ -2113,7 +2086,7 @@ extern "C" int rrt_get_proof_audit(rrt_ctx* c, uint64_t* out) {
   for (int k = 0; k < 2 * RRT_AUDIT_KINDS; ++k) out[k] = 0;
   if (!c->d_audit) return RRT_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  uint32_t h[16];
+  unsigned long long h[16];
   HIPCHK(c, hipDeviceSynchronize());
   HIPCHK(c, hipMemcpy(h, c->d_audit, sizeof(h), hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemset(c->d_audit, 0, sizeof(h)));

@@ -141,12 +141,6 @@ struct DShadowProof {
   double w[6];            // host: the kept triangles' largest vertex distance from their face
   uint32_t n[6];
   uint32_t on, pad;
-  // camera-ray hit proof (rrt_device.h camera_hit_proof): bit i of emit[f] = kept triangle i of face
-  // f is a light (a hit on it is not black); every other primitive of the scene lies in the box
-  // [nocc_lo, nocc_hi] (lo > hi: none); hit_on enables the proof (the area-light build)
-  uint32_t emit[6];
-  uint32_t hit_on, hit_pad;
-  double nocc_lo[3], nocc_hi[3];
 };
 
 // Kerr shadow-ray occlusion proof (rrt_device.h kerr_occluded_proof): a coarse march
@@ -170,18 +164,10 @@ struct DKerrProof {
 // tile_order[ix / ts^2], then claim_r(ix % ts^2) = the pixel's row-major index in the tile): 8x8
 // blocks in row-major order, row-major inside each (ts is a multiple of 8), so 64 consecutive
 // claims -- a wave of the pixel pass, a strip of its first level -- are a square of pixels.
-// 0: row-major claims (A/B).
-#ifndef RRT_CLAIM_BLOCK8
-#define RRT_CLAIM_BLOCK8 1
-#endif
+// (Row-major claims measured slower: profiles/r04_ab_claim_block8.txt.)
 __host__ __device__ __forceinline__ uint32_t claim_r(uint32_t c, uint32_t ts) {
-#if RRT_CLAIM_BLOCK8
   const uint32_t b = c >> 6, w = c & 63u, nb = ts >> 3;
   return ((b / nb) * 8u + (w >> 3)) * ts + (b % nb) * 8u + (w & 7u);
-#else
-  (void)ts;
-  return c;
-#endif
 }
 
 #define RRT_MAX_QUEUES 8
@@ -276,7 +262,7 @@ struct KParams {
   // batch kernel: a wave whose oldest pixel has run this long (wall-clock ticks, 100 MHz) takes
   // issue priority 2, four times as long priority 3 (rrt_sample.hip tail_prio)
   uint32_t prio_ticks;
-  uint32_t deal;  // batch kernel: dealt shadow walks (rrt_sample.hip shadow_dealt); RRT_AB_NO_DEAL=1 turns them off
+  uint32_t prio_pad;
   DKerrProof kproof;      // Kerr builds: the shadow rays' occlusion proof (kp.occ's face triangles)
   // the pixel pass's first level (rrt_strip_proof_kernel): strips of 64 consecutive claim indices
   // proven as wholes -- flag 1 per strip -- before the per-pixel level (null: per-pixel pass only)
@@ -284,7 +270,7 @@ struct KParams {
   // run-time proof audit (rrt_device.h audit_pick): counting launches re-check every
   // 2^audit_shift-th proven ray (and pixel) against the exact march; tallies [2 k] checked,
   // [2 k + 1] violations per proof k (RRT_AUDIT_*); null: no audit
-  uint32_t* audit;
+  unsigned long long* audit;  // 64-bit: a 1080p frame audited at every_log2 = 0 exceeds 2^32 checks
   uint32_t audit_shift, audit_pad;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by

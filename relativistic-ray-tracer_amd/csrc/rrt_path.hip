@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_path_kernel(const KParams* __r
       bool known = false;
       if (cray) {
         known = camera_proven_miss<false, false>(kp, o, d, cn);
-      } else if (any && RRT_SHADOW_PROOF && kp.occ.on) {
+      } else if (any && kp.occ.on) {
         h = shadow_occluded_proof<RRT_OCC_TAG_PATH(WAVES)>(kp, o, d, kp.hole.steps);
         known = h;
       }

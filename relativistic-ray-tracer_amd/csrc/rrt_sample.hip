@@ -49,7 +49,7 @@ __device__ __forceinline__ void park_hit(SL& cl, uint32_t t, const Isect& is0) {
 // estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
 // W: the calling kernel build's tag for the out-of-line occlusion proof (rrt_device.h query_nx)
-template <bool COUNT, int LEAN, bool NI = false, int W = 0, class SL = ShadeLds>
+template <bool COUNT, int LEAN, int W = 0, class SL = ShadeLds>
 __device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
@@ -70,7 +70,7 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint
       const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
       // only the loop state and the RNG stay in registers across the shadow query
       lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
-      if (!query_nx<true, COUNT, NI, LEAN == V_KERR, W, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
+      if (!query_nx<true, COUNT, LEAN == V_KERR, W, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, nullptr, cn))
         L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
     }
   }
@@ -80,11 +80,11 @@ template <bool COUNT, int LEAN, int W = 0>
 __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
-  return direct_importance_parked<COUNT, LEAN, false, W>(kp, g, cl, t, cn);
+  return direct_importance_parked<COUNT, LEAN, W>(kp, g, cl, t, cn);
 }
 
 // estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
-template <bool COUNT, int LEAN, bool NI = false>
+template <bool COUNT, int LEAN>
 __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   const int num = (int)(kp.n_lights * kp.ns_area_light);
@@ -98,7 +98,7 @@ __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl
     const v3 wi_world = to_world(f, w_in);
     const spec fw = bsdf_f(kp.bsdfs[bsdf], to_local(f, wo), w_in);
     Isect is2;
-    if (query_nx<false, COUNT, NI, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
+    if (query_nx<false, COUNT, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, hp + smul(EPS_D, wi_world), wi_world, &is2, cn))
       L = L + (emission(kp.bsdfs[is2.bsdf]) * fw) * (float)w_in.z;
   }
   return ((L * 2.0f) * (float)PI_D) / (float)num;
@@ -108,187 +108,6 @@ __device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is
                                       Counters& cn) {
   park_hit(cl, t, is0);
   return direct_hemisphere_parked<COUNT, LEAN>(kp, g, cl, t, cn);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Zero samples.  A camera ray that camera_hit_proof shows to hit a non-emitting face
-// triangle of the room near Q, and whose every light sample's shadow ray from Q the occlusion proof
-// shows occluded, renders +0: emission 0 (est_radiance_global_illumination, part1_code.cpp:103-123)
-// plus direct light 0 -- an occluded sample adds nothing (part1_code.cpp:52-55), whatever its BSDF
-// value, pdf or cosine -- with the hit's draws (the light samples draw the same numbers from the
-// slot's stream).  Q lies within the recurrence's deviation (tools/hit_proof_sweep.py: < 2e-13) of the
-// reference's hit point, so the shadow proofs run with RRT_ZERO_MS times the margins.  The batch
-// kernel then skips the sample's exact camera march and its shading.  g: the slot's stream after
-// the jitter draws.
-#ifndef RRT_ZERO_MS
-#define RRT_ZERO_MS 2.0
-#endif
-#define RRT_ZERO_BSDF 0xffffffffu  // the parked record of a zero sample (no shading)
-template <int LEAN, int W>
-__device__ __forceinline__ bool zero_sample_proof(const KParams& kp, v3 o, v3 d, Rng g) {
-  v3 Q;
-  if (!camera_hit_proof(kp, o, d, Q)) return false;
-  if (kp.max_ray_depth == 0) return true;
-  for (uint32_t li = 0; li < kp.n_lights; ++li) {
-    const int num = kp.lights[li].is_delta ? 1 : (int)kp.ns_area_light;
-    for (int i = 0; i < num; ++i) {
-      v3 wi;
-      float dist, pdf;
-      (void)light_sample_L<LEAN>(kp.env, kp.lights[li], g, Q, wi, dist, pdf);
-      if (!shadow_occluded_proof<W>(kp, Q + smul(EPS_D, wi), wi, kp.hole.steps, RRT_ZERO_MS)) return false;
-    }
-  }
-  return true;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Segment-parallel shadow queries ("dealt walks").  BVHAccel::intersect
-// (bvh.cpp:103-113) marches a chain of micro segments; each segment depends only on the one before
-// (BlackHole::next_micro_ray, blackhole.cpp:17-40), never on a walk's result, and a shadow query is
-// true iff some segment before the capture hits a primitive.  So the chain can be generated first
-// and its walks run in any order, by any lanes.  In the batch kernel a wave's unproven shadow rays
-// are few (the occlusion proof takes most), and marched lane by lane their walks run one micro step
-// at a time while the wave's other lanes idle.  Here the wave's rays generate their chains in
-// lock-step, the segments that need a walk (not captured before, not skipped: outside the root box
-// or in clear grid cells) go to a per-wave LDS list, and when the list is full (or every chain has
-// ended) each lane of the wave walks one listed segment; a ray stops generating once one of its
-// walks has hit.  The answer is the reference's: hit <=> some uncaptured segment's walk hits.
-#ifndef RRT_DEAL
-#define RRT_DEAL 0  // 1: build with the dealt shadow walks (A/B: slower, DESIGN.md §5 -- cfg3 15.45 ms without,
-                    // 16.56 ms with shadow_dealt inlined, 17.44 ms out of line; no gain on the 8-way split)
-#endif
-#ifndef RRT_ZERO
-#define RRT_ZERO 0  // 1: build with the zero samples in the batch kernel (A/B: slower, DESIGN.md §5 -- cfg3
-                    // 19.1-19.5 ms with, 15.5 ms without; the proof's registers raise the kernel's spills
-                    // 161 -> 272 VGPRs and its saved marches do not shorten the waves that run them)
-#endif
-#ifndef RRT_DEAL_CAP
-#define RRT_DEAL_CAP 32  // listed segments per wave (LDS: 60 B each)
-#endif
-template <uint32_t CAP>
-struct DealLds {  // per wave: micro segments waiting for a walk (structure of arrays)
-  double o[3][CAP], d[3][CAP], mt[CAP];
-  uint32_t ray[CAP];
-  unsigned long long occ;  // lanes whose query found a hit
-};
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-// The shadow query (BVHAccel::intersect without an Intersection) of every lane with need set;
-// all 64 lanes of the wave call it together.  Returns the query's result for those lanes.
-#ifndef RRT_DEAL_INLINE
-#define RRT_DEAL_INLINE 0  // 1: shadow_dealt inlined into the batch kernel (A/B)
-#endif
-#if RRT_DEAL_INLINE
-#define RRT_DEAL_ATTR __forceinline__
-#else
-#define RRT_DEAL_ATTR __noinline__
-#endif
-template <uint32_t CAP>
-__device__ RRT_DEAL_ATTR bool shadow_dealt(const KParams& kp, v3 o, v3 d, bool need, DealLds<CAP>& dl, uint32_t lane) {
-  static_assert(CAP <= 64, "one listed segment per lane and drain");
-  if (__ballot(need) == 0) return false;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (lane == 0) lput(&dl.occ, 0u, 0ull);
-  wave_sync_lds();
-  v3 e = o;
-  double max_t = 0.0;
-  int j = 0;
-  bool gen = need;
-#pragma unroll 1
-  for (;;) {
-    uint32_t n = 0;  // listed segments (wave-uniform)
-    // generate: the chains one micro step per pass -- as many of them as the list has room for a
-    // segment of (the first generating lanes), the others wait for the next pass
-#pragma unroll 1
-    for (;;) {
-      const uint64_t gm = __ballot(gen);
-      if (gm == 0 || n == CAP) break;
-      const bool step = gen && (uint32_t)__popcll(gm & lt) < CAP - n;
-      bool want = false;
-      if (step) {
-        v3 rel;
-        double rel2;
-        next_micro_at(kp.hole, e, o, d, max_t, rel, rel2);
-        ++j;
-        if (sphere_t_rel(rel, rel2, kp.hole.r2, d, max_t)) {  // captured: the query ends without a hit
-          gen = false;
-        } else {
-          e = o + vmul(d, max_t);
-          want = !segment_outside_root(kp, o, e) && !cell_clear(kp.grid, grid_cell(kp.grid, o), max_t);
-          if (j >= kp.hole.steps) gen = false;
-        }
-      }
-      const uint64_t wm = __ballot(want);
-      if (want) {
-        const uint32_t k = n + (uint32_t)__popcll(wm & lt);
-        lput(dl.o[0], k, o.x); lput(dl.o[1], k, o.y); lput(dl.o[2], k, o.z);
-        lput(dl.d[0], k, d.x); lput(dl.d[1], k, d.y); lput(dl.d[2], k, d.z);
-        lput(dl.mt, k, max_t); lput(dl.ray, k, lane);
-      }
-      n += (uint32_t)__popcll(wm);
-    }
-    if (n == 0) break;  // every chain has ended and nothing is listed
-    wave_sync_lds();
-    // drain: lane k walks listed segment k (a ray already known to hit is skipped)
-    if (lane < n) {
-      const uint32_t r = lget(dl.ray, lane);
-      if (!((lget(&dl.occ, 0u) >> r) & 1ull)) {
-        const v3 so = V(lget(dl.o[0], lane), lget(dl.o[1], lane), lget(dl.o[2], lane));
-        const v3 sd = V(lget(dl.d[0], lane), lget(dl.d[1], lane), lget(dl.d[2], lane));
-        const double smt = lget(dl.mt, lane);
-        Counters cn = {};
-        if (segment_walk<true, false>(kp, so, sd, smt, so + vmul(sd, smt), grid_cell(kp.grid, so), nullptr, cn))
-          atomicOr(&dl.occ, 1ull << r);
-      }
-    }
-    wave_sync_lds();
-    if ((lget(&dl.occ, 0u) >> lane) & 1ull) gen = false;  // a hit: the query is true
-    if (__ballot(gen) == 0) break;
-  }
-  return need && ((lget(&dl.occ, 0u) >> lane) & 1ull);
-}
-
-// estimate_direct_lighting_importance (part1_code.cpp:33-57) for the hit parked in LDS, with every
-// lane of the wave taking part (act: this lane shades a hit): the occlusion proof per lane, then the
-// unproven shadow rays through shadow_dealt.  Same draws, same sums as direct_importance_parked.
-template <int LEAN, int W, uint32_t CAP, class SL>
-__device__ spec direct_importance_wave(const KParams& kp, Rng& g, SL& cl, uint32_t t, bool act, DealLds<CAP>& dl) {
-  const uint32_t lane = t & 63u;
-  spec L = S(0, 0, 0);
-  int total = 0;
-  for (uint32_t li = 0; li < kp.n_lights; ++li) {
-    const uint32_t is_delta_l = kp.lights[li].is_delta;
-    const int num = is_delta_l ? 1 : (int)kp.ns_area_light;
-    total += num;
-    for (int i = 0; i < num; ++i) {
-      bool need = false;
-      v3 so = V(0.0, 0.0, 0.0), sd = V(0.0, 0.0, 1.0);
-      if (act) {
-        const uint32_t bsdf = lget(cl.bsdf, t);
-        const v3 hp = V(lget(cl.hp[0], t), lget(cl.hp[1], t), lget(cl.hp[2], t));
-        const v3 nn = V(lget(cl.nn[0], t), lget(cl.nn[1], t), lget(cl.nn[2], t));
-        const v3 wo = V(lget(cl.wo[0], t), lget(cl.wo[1], t), lget(cl.wo[2], t));
-        v3 wi_world; float dist, pdf;
-        const spec sample = light_sample_L<LEAN>(kp.env, kp.lights[li], g, hp, wi_world, dist, pdf);
-        const Frame f = coord_space(nn);
-        const v3 w_in = to_local(f, wi_world);
-        if (!(w_in.z < 0)) {
-          const spec contrib = ((sample * bsdf_f<LEAN>(kp.bsdfs[bsdf], to_local(f, wo), w_in)) * (float)w_in.z) / pdf;
-          lput(cl.cr, t, contrib.r); lput(cl.cg, t, contrib.g); lput(cl.cb, t, contrib.b);
-          so = hp + smul(EPS_D, wi_world);
-          sd = wi_world;
-          // the occlusion proof first (rrt_device.h query_nx): a proven ray is occluded
-          need = !(RRT_SHADOW_PROOF && W && kp.occ.on && shadow_occluded_proof<W>(kp, so, sd, kp.hole.steps));
-        }
-      }
-      const bool occluded = shadow_dealt<CAP>(kp, so, sd, need, dl, lane);
-      if (need && !occluded) L = L + S(lget(cl.cr, t), lget(cl.cg, t), lget(cl.cb, t));
-    }
-  }
-  return L / (float)total;
 }
 
 }  // namespace rrt
@@ -432,7 +251,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
               (rrt_mix64(g.key) & ((1ull << kp.audit_shift) - 1ull)) == 0ull) {
             if (pixel_miss_proof(kp, x, y)) aud |= 1u;
             const uint32_t sx = kp.tiles[2 * tl] + (lx & ~7u), sy = kp.tiles[2 * tl + 1] + (ly & ~7u);
-            if (RRT_CLAIM_BLOCK8 && sx >= kp.clip_x0 && sy >= kp.clip_y0 && sx + 8u <= kp.clip_x1 && sy + 8u <= kp.clip_y1 &&
+            if (sx >= kp.clip_x0 && sy >= kp.clip_y0 && sx + 8u <= kp.clip_x1 && sy + 8u <= kp.clip_y1 &&
                 rect_miss_proof(kp, (double)sx, (double)sy, 8.0, 8.0))
               aud |= 2u;
           }
@@ -459,14 +278,11 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
     const double vx = (1 - cx) * cam.blx + cx * -cam.blx, vy = (1 - cy) * cam.bly + cy * -cam.bly;
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     spec s = S(0, 0, 0);
-    const Rng g_jit = g;  // the stream after the jitter (the zero-sample audit's light samples)
     {
       Isect is;
       const v3 wd = unit(w);
-      bool hitq = false;
       if (!camera_proven_miss<COUNT, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn) &&
           query<false, COUNT, LEAN == V_KERR, is_lean(LEAN)>(kp, ld3(cam.pos), wd, &is, cn)) {  // est_radiance (:103-123)
-        hitq = true;
         const spec e = emission(kp.bsdfs[is.bsdf]);
         if (kp.max_ray_depth == 0) s = e;
         else if (DEEP && kp.max_ray_depth >= 2) s = e + at_least_one_bounce<COUNT, general_of(LEAN)>(kp, g, is, cn);
@@ -475,13 +291,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
         else s = e + direct_importance_lds<COUNT, LEAN, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, g, is, cl, t, cn);
       } else if (!is_lean(LEAN) && kp.env.w) {
         s = env_dir(kp.env, unit(w));  // miss: envLight->sample_dir of the unbent camera ray
-      }
-      // audit of the zero samples (the batch kernel's area-light build): a proven zero sample must be
-      // a hit whose radiance is +0 here, where it is marched and shaded exactly
-      if (COUNT && kp.audit && kp.occ.hit_on && LEAN != V_KERR && audit_pick(kp, ld3(cam.pos), wd) &&
-          zero_sample_proof<0, RRT_OCC_TAG_S(COUNT, LEAN, WAVES)>(kp, ld3(cam.pos), wd, g_jit)) {
-        const bool ok = hitq && s.r == 0.0f && s.g == 0.0f && s.b == 0.0f && !signbit(s.r) && !signbit(s.g) && !signbit(s.b);
-        audit_note(kp, RRT_AUDIT_ZERO, !ok);
       }
       if (COUNT && aud) {  // the pixel pass's proofs say this camera ray misses
         Counters c2 = {};
@@ -558,14 +367,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_sample_kernel(const KParams* _
 // group leader folds the samples into the pixel sums in sample order (the reference's float /
 // double accumulation order) with the adaptive stop test at every samples_per_batch boundary;
 // samples past the stop are discarded with their draws.  Results equal the sequential loop's.
-#ifndef RRT_BATCH_CALL
-#define RRT_BATCH_CALL 0  // 1: geodesic queries out of line in the batch kernel (register A/B)
-#endif
-#ifndef RRT_KERR_CALL
-#define RRT_KERR_CALL 0  // 1: the Kerr build's queries out of line in the batch kernel (register A/B)
-#endif
-#define RRT_BCALL(LEAN) (RRT_BATCH_CALL || ((LEAN) == V_KERR && RRT_KERR_CALL))
-
 // draw-offset slots per group and step: a hit takes Dh / Dm slots (2 with one area light, the
 // LEAN builds; 3 with an environment light too), so 32 samples need up to 31 * (Dh / Dm) + 1
 template <int LEAN>
@@ -573,21 +374,7 @@ struct SlotWindow { static constexpr uint32_t n = rrt::is_lean(LEAN) ? 64u : 128
 // striped claim queues: runs of RRT_STRIPE_OF(V) consecutive claims (neighbouring pixels).
 // Interleaved A/B (ms/frame): cfg3 (build 1) 20.2 at 32, 20.7 at 16, 20.7 at 8; cfg4 (build 2)
 // 20.6 at 32, 20.0 at 16.
-#ifndef RRT_STRIPE
 #define RRT_STRIPE_OF(V) ((V) == 2 ? 16u : 32u)
-#else
-#define RRT_STRIPE_OF(V) ((uint32_t)RRT_STRIPE)
-#endif
-#ifndef RRT_CLAIM_HYP
-#define RRT_CLAIM_HYP 2  // a listed pixel's first step speculates 0: "miss"; 1: "hit"; 2: the pixel
-                         // proof pass's hint (A/B: cfg3 23.9 / 22.6 / 20.5 ms, cfg4 - / 19.8 / 20.1)
-#endif
-#ifndef RRT_TAIL_PRIO
-#define RRT_TAIL_PRIO 1   // 0: no wave priority boost for long-running pixels (A/B)
-#endif
-#ifndef RRT_PRIO_TICKS
-#define RRT_PRIO_TICKS 50000  // 0.5 ms of wall clock (100 MHz): a long-running pixel (KParams::prio_ticks)
-#endif
 
 // Per-group pixel state, cold during the queries: kept in LDS (one slot per group) so the walks
 // run with only the lane's own few speculation registers live.
@@ -652,14 +439,14 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
     const v3 wd = unit(w);
     Isect is;
     const bool hit = !camera_proven_miss<false, false>(kp, ld3(cam.pos), wd, cn) &&
-                     query_nx<false, false, RRT_BATCH_CALL, false>(kp, ld3(cam.pos), wd, &is, cn);
+                     query_nx<false, false, false>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (hit) {
       park_hit(hl.sh, t, is);
       g.ctr = sl * Dm + Dm;
       const spec e = emission(kp.bsdfs[lget(hl.sh.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else s = e + direct_importance_parked<false, LEAN, RRT_BATCH_CALL, W>(kp, g, hl.sh, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, W>(kp, g, hl.sh, t, cn);
     }
     const uint64_t hb = __ballot(hit);
     if ((t & 63u) == 0) hl.hits[t >> 6] = hb;
@@ -775,12 +562,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   // the claim space (a multiple of 64 pixels: tiles of 8k x 8k) must hold whole stripes
   static_assert(STRIPE > 0 && 64u % STRIPE == 0, "RRT_STRIPE must divide 64");
   __shared__ GroupLds<RRT_SLOTS> gs;
-  // the area-light build at <= 4 waves/SIMD (LDS: 4 blocks of 28.5 + 7.7 KB a CU); not the point-light
-  // build (no occlusion proof, few shadow rays: cfg4's frame is its camera rays)
-  constexpr bool DEAL = RRT_DEAL && LEAN == 1 && WAVES <= 4;
-  constexpr bool ZERO = RRT_ZERO && LEAN == 1;  // zero samples (zero_sample_proof): the area-light build
-  constexpr uint32_t DCAP = DEAL ? (uint32_t)RRT_DEAL_CAP : 1u;
-  __shared__ DealLds<DCAP> dl[4];  // one per wave (shadow_dealt)
   float* const fr = cl.cr;  // per-lane sample radiance for the ordered fold (free after shading)
   float* const fg = cl.cg;
   float* const fb = cl.cb;
@@ -909,9 +690,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
             } else {
               lput(gs.O, gid, 0u); lput(gs.i, gid, 0u);
               // The first step's hypothesis: "miss" without the pixel proof's list; for a listed
-              // pixel (one whose camera rays are not all proven misses) RRT_CLAIM_HYP 1 takes
-              // "hit", 2 the list entry's hint (its central ray is no proven miss)
-              const uint32_t hyp0 = !kp.claim_list ? 0u : RRT_CLAIM_HYP == 2 ? (ent >> 31) : RRT_CLAIM_HYP ? 1u : 0u;
+              // pixel (one whose camera rays are not all proven misses) the list entry's hint (its
+              // central ray is no proven miss).  A/B: "miss" / "hit" / hint for every listed pixel:
+              // cfg3 23.9 / 22.6 / 20.5 ms, cfg4 - / 19.8 / 20.1
+              const uint32_t hyp0 = !kp.claim_list ? 0u : (ent >> 31);
               lput(gs.hyp, gid, hyp0);
               lput(gs.rr, gid, 0.0f); lput(gs.rg, gid, 0.0f); lput(gs.rb, gid, 0.0f);
               lput(gs.s1, gid, 0.0); lput(gs.s2, gid, 0.0);
@@ -932,7 +714,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     // whose oldest pixel has been running for a while takes issue priority over the other waves
     // of its SIMD, so the costliest pixels finish early instead of forming the frame's tail.
     auto tail_prio = [&]() {
-      if (!RRT_TAIL_PRIO) return;
       const uint64_t age = have ? wall_clock64() - t_claim : 0;
       if (__ballot(age > 4ull * kp.prio_ticks)) __builtin_amdgcn_s_setprio(3);
       else if (__ballot(age > kp.prio_ticks)) __builtin_amdgcn_s_setprio(2);
@@ -976,11 +757,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
       const v3 wd = unit(w);
       if (camera_proven_miss<false, LEAN == V_KERR>(kp, ld3(cam.pos), wd, cn)) return false;
-      if (ZERO && kp.occ.hit_on && zero_sample_proof<LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, ld3(cam.pos), wd, g)) {
-        is->bsdf = (int)RRT_ZERO_BSDF;  // a hit whose radiance is +0: no record, no shading
-        return true;
-      }
-      return query_nx<false, false, RRT_BCALL(LEAN), LEAN == V_KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, is, cn);
+      return query_nx<false, false, LEAN == V_KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, is, cn);
     };
     const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;  // this group's lanes
     const uint64_t lt = ((1ull << lane) - 1ull) & gmask;                         // group lanes before me
@@ -1105,20 +882,13 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
       const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
       s = env_dir(kp.env, unit(w));
     }
-    const bool zero = ZERO && act && hit && lget(cl.bsdf, t) == RRT_ZERO_BSDF;  // radiance +0
-    if (DEAL && kp.deal && kp.max_ray_depth != 0) {
-      // every lane takes part: the unproven shadow rays' walks are dealt over the wave (shadow_dealt)
-      const bool shade = act && hit && !zero;
-      Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
-      const spec dsum = direct_importance_wave<LEAN, RRT_OCC_TAG(LEAN, WAVES), DCAP>(kp, g, cl, t, shade, dl[t >> 6]);
-      if (shade) s = emission(kp.bsdfs[lget(cl.bsdf, t)]) + dsum;
-    } else if (act && hit && !zero) {
+    if (act && hit) {
       Rng g; g.key = lget(gs.key, gid); g.ctr = off + Dm;
       const spec e = emission(kp.bsdfs[lget(cl.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_BCALL(LEAN), RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN, RRT_BCALL(LEAN)>(kp, g, cl, t, cn);
-      else s = e + direct_importance_parked<false, LEAN, RRT_BCALL(LEAN), RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
+      else if (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
+      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN>(kp, g, cl, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, RRT_OCC_TAG(LEAN, WAVES)>(kp, g, cl, t, cn);
     }
     if (act) { lput(fr, t, s.r); lput(fg, t, s.g); lput(fb, t, s.b); }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1232,21 +1002,6 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
 // samples_per_batch) and count * draws_miss draws -- written here.  The others go to the claim
 // list, appended per wave (one atomic) so claims keep their order within each wave's run.
 // Claim index ix of the pass (a whole wave calls it together: ballots and one atomic per wave).
-#ifndef RRT_HEAVY_STRADDLE
-#define RRT_HEAVY_STRADDLE 0  // 1: listed pixels with a proven-miss corner ray go to the heavy list too (A/B)
-#endif
-// A listed pixel (not every ray a proven miss) one of whose corner rays is a proven miss straddles
-// the scene's silhouette: its samples mix hits and misses, the costliest case of the batch kernel's
-// slot speculation (several rounds per step).  A routing heuristic only, like pixel_heavy.
-__device__ __forceinline__ bool pixel_straddles(const KParams& kp, uint32_t x, uint32_t y) {
-  using namespace rrt;
-  Counters cn = {};
-  bool any = false;
-#pragma unroll 1
-  for (int k = 0; k < 4 && !any; ++k)
-    any = camera_miss_proof<false>(kp, ld3(kp.cam.pos), pixel_ray_dir(kp, (double)x + (k & 1), (double)y + (k >> 1)), cn);
-  return any;
-}
 __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, uint32_t lane) {
   using namespace rrt;
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
@@ -1262,7 +1017,7 @@ __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, u
         if (kp.draws) kp.draws[slot] = n * kp.draws_miss;
       } else {
         listed = true;
-        heavy = kp.heavy_list && (pixel_heavy(kp, x, y) || (RRT_HEAVY_STRADDLE && pixel_straddles(kp, x, y)));
+        heavy = kp.heavy_list && pixel_heavy(kp, x, y);
       }
     }
   }
@@ -1278,10 +1033,10 @@ __device__ __forceinline__ void pixel_pass_one(const KParams& kp, uint32_t ix, u
       listed = false;
     }
   }
-  // RRT_CLAIM_HYP 2: a listed pixel's hint bit (31) = its central camera ray is no proven miss
-  // (the batch kernel's first hypothesis for the pixel)
+  // a listed pixel's hint bit (31) = its central camera ray is no proven miss (the batch kernel's
+  // first hypothesis for the pixel)
   uint32_t hint = 0u;
-  if (RRT_CLAIM_HYP == 2 && listed) {
+  if (listed) {
     const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
     const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
     Counters cn = {};
@@ -1330,7 +1085,7 @@ __global__ __launch_bounds__(256) void rrt_strip_proof_kernel(const KParams* __r
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   if (s < kp.n_pixels / 64u) {
     const uint32_t ix0 = s * 64u, tl = kp.tile_order[ix0 / tpix], r0 = claim_r(ix0 % tpix, ts);
-    const uint32_t w = RRT_CLAIM_BLOCK8 ? 8u : ts < 64u ? ts : 64u, hh = 64u / w;
+    const uint32_t w = 8u, hh = 8u;
     const uint32_t x = kp.tiles[2 * tl] + r0 % ts, y = kp.tiles[2 * tl + 1] + r0 / ts;
     const bool inside = x >= kp.clip_x0 && y >= kp.clip_y0 && x + w <= kp.clip_x1 && y + hh <= kp.clip_y1;
     if (inside && rect_miss_proof(kp, (double)x, (double)y, (double)w, (double)hh)) {

@@ -64,8 +64,7 @@ def test_audit_schwarzschild_proofs(gpu, name, region, misses):
     assert np.array_equal(a0[0].view(np.uint32), ref.view(np.uint32))  # the reference's frame
     if misses:
         assert t["camera"]["checked"] > 0 and t["pixel"]["checked"] > 0 and t["strip"]["checked"] > 0, t
-    if name.startswith("cfg3") and region[0] > 0:  # the room: zero samples (camera hit + occlusion proofs)
-        assert t["zero"]["checked"] > 0, t
+    assert t["zero"]["checked"] == 0, t  # reserved kind: no zero-sample proof in the product
     assert sum(v["checked"] for v in t.values()) > 0, t
     assert all(v["violations"] == 0 for v in t.values()), t
 

@@ -4,8 +4,13 @@ interleaved rounds in one process; prints the HIP-event kernel time per variant.
 Usage: python3 tools/ab_workload.py --workload cfg5 --rounds 2 3 4 5   (VARIANT, VARIANT:FLAGS or
 VARIANT:FLAGS:RRT_AB_X=V,... -- library A/B switches the launch reads from the environment)
 --world N: time each of the N ranks' tile sets (bench.py's block-cyclic split) on this one GPU and
-report the slowest rank per variant (the N-GPU frame's kernel time, without the gather)."""
+report the slowest rank per variant (the N-GPU frame's kernel time, without the gather).
+Outputs: every rank's packed buffer is poisoned (NaN radiance, count -1) before its launch and
+unpacked into a full frame (itself poisoned per variant); variants are compared by the SHA-256 of
+that frame's bits ("identical_outputs"), and the frame is checked bit for bit against the
+workload's reference goldens where it has them ("verified", bench.verify_frame)."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -49,8 +54,10 @@ def main():
     n = max(len(t) for t in sets) * ts * ts
     prgb = torch.zeros(n * 3, dtype=torch.float32, device="cuda")
     pcnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    frgb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    fcnt = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    times, sums = {v: [] for v in a.variants}, {}
+    times, sums, digests, verified = {v: [] for v in a.variants}, {}, {}, {}
     per_rank = {v: [[] for _ in sets] for v in a.variants}
     for _ in range(a.rounds):
         for v in a.variants:
@@ -63,22 +70,34 @@ def main():
                 k, _, val = kv.partition("=")
                 os.environ[k] = val
             p = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1), variant=int(var), flags=int(fl or 0))
-            worst, tot_rgb, tot_cnt = 0.0, 0.0, 0
+            worst = 0.0
+            frgb.view(torch.int32).fill_(-1)
+            fcnt.fill_(-1)
             for k, tiles in enumerate(sets):
+                prgb.view(torch.int32).fill_(-1)  # poison: stale slots of an earlier rank cannot leak
+                pcnt.fill_(-1)
                 r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
                 torch.cuda.synchronize()
                 ms = r.stats().last_kernel_ms
                 per_rank[v][k].append(ms)
                 worst = max(worst, ms)
-                m = len(tiles) * ts * ts
-                tot_rgb += float(prgb[:3 * m].double().sum().item())
-                tot_cnt += int(pcnt[:m].long().sum().item())
+                r.unpack_tiles_device(tiles, ts, W, H, prgb.data_ptr(), pcnt.data_ptr(), frgb.data_ptr(),
+                                      fcnt.data_ptr(), stream=s)
+            torch.cuda.synchronize()
             times[v].append(worst)
-            sums[v] = (tot_rgb, tot_cnt)
+            fr, fc = frgb.cpu().numpy(), fcnt.cpu().numpy()
+            sums[v] = (float(fr.astype(np.float64).sum()), int(fc.astype(np.int64).sum()))
+            dg = hashlib.sha256(fr.tobytes() + fc.tobytes()).hexdigest()[:16]
+            if digests.setdefault(v, dg) != dg:
+                digests[v] = "varies"  # a variant whose rounds differ: not deterministic
+            if v not in verified:
+                verified[v] = bench.verify_frame(a.workload, fr.reshape(H, W, 3), fc.reshape(H, W))
             print(v, times[v][-1], r.stats().kernel.decode(), flush=True)
     # diagnostic flags change outputs; environment switches (third field) do not
-    same = len(set(s for v, s in sums.items() if v.split(":")[1:2] in ([], ["0"], [""]))) <= 1
-    print(json.dumps({"workload": a.workload, "identical_outputs": same,
+    plain = [d for v, d in digests.items() if v.split(":")[1:2] in ([], ["0"], [""])]
+    same = len(set(plain)) <= 1 and "varies" not in plain
+    print(json.dumps({"workload": a.workload, "identical_outputs": same, "digests": digests,
+                      "verified": {v: x[0] for v, x in verified.items()},
                       "median_ms": {v: float(np.median(t)) for v, t in times.items()},
                       **({"world": a.world, "rank_median_ms": {v: [float(np.median(x)) for x in pr] for v, pr in per_rank.items()}}
                          if a.world > 1 else {}),
