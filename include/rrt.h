@@ -26,13 +26,15 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 4  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
+#define RRT_ABI_VERSION 5  /* 2: rrt_spacetime_desc gained spin + axis (Kerr)
                               3: rrt_stats gained last_main_kernel_ms / last_heavy_pixels (callers
                                  built against 2 pass a smaller struct: rebuild), the
                                  RRT_RENDER_WAVEFRONT selects the path pool kernel (depth >= 2;
                                  RRT_E_INVALID elsewhere),
                                  rrt_libm_eval added
-                              4: rrt_set_proof_audit / rrt_get_proof_audit added */
+                              4: rrt_set_proof_audit / rrt_get_proof_audit added
+                              5: rrt_stats gained last_cont_pixels (continuations); the proof-audit
+                                 tallies are 64-bit on the device too */
 
 enum {
   RRT_OK = 0,
@@ -321,6 +323,8 @@ typedef struct {
   float last_main_kernel_ms;  /* HIP-event time of the last launch's main kernel alone (after
                                  any pre-pass such as rrt_pixel_proof_kernel) */
   uint32_t last_heavy_pixels;  /* pixels the last launch rendered slot-parallel (heavy pixels) */
+  uint32_t last_cont_pixels;   /* pixels the last launch's batch kernel handed to the heavy kernel
+                                  between adaptive steps (continuations) */
 } rrt_stats;
 int rrt_get_stats(const rrt_ctx* ctx, rrt_stats* out);
 /* Diagnostics: evaluate the device's restatement of the host C library's transcendentals

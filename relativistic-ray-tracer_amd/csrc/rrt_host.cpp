@@ -33,7 +33,7 @@ hipError_t rrt_launch_sample(const KParams& kp, const KParams* d_kp, int count, 
 hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_first(const KParams& kp, const KParams* d_kp, int lean, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_pixel_proof(const KParams* d_kp, uint32_t n_pixels, bool strips, hipStream_t stream);
-hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream);
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, int drain, hipStream_t stream);
 hipError_t rrt_launch_path(const KParams* d_kp, int waves, uint32_t grid, hipStream_t stream);
 hipError_t rrt_launch_unpack(const uint32_t* tiles, uint32_t n_tiles, uint32_t ts, uint32_t fw, uint32_t fh,
                              const float* rgb_p, const int32_t* cnt_p, float* rgb, int32_t* cnt, hipStream_t stream);
@@ -44,7 +44,8 @@ hipError_t rrt_launch_tonemap(uint32_t n, const float* rgb, uint32_t* out, float
 namespace {
 
 constexpr double kPI = 3.14159265358979323;  // CGL misc.h:11
-constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);  // claim counters + the pixel proof's list length + the heavy list's
+// claim counters + the pixel proof's list length + the heavy list's + the continuation queue's
+constexpr size_t kCounterBytes = sizeof(uint32_t) * RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2 + RRT_CONT_WORDS);
 // Heavy pixels (rrt_sample.hip heavy_pixel_block): rays passing within RRT_HEAVY_NEAR r_s of the hole (or straddling
 // its capture boundary) make a pixel heavy (profiles/r03_heavy_ab.md)
 #define RRT_HEAVY_NEAR 1.2
@@ -127,6 +128,9 @@ struct rrt_ctx {
   uint32_t audit_shift = 0;          // 0: no audit; else re-check every 2^(audit_shift - 1)-th proven ray
   size_t strip_list_cap = 0;
   size_t heavy_list_cap = 0;
+  ContRec* d_cont = nullptr;  // continuation records (rrt_sample.hip cont_push)
+  size_t cont_cap = 0;
+  uint32_t cont_seq = 0;      // the last launch's record tag (never 0)
   float* d_path_stack = nullptr;  // the path pool kernel's per-level terms (rrt_path.hip)
   size_t path_stack_cap = 0;      // bytes
   hipStream_t side = nullptr;  // the heavy pixels' kernel runs here, beside the batch kernel
@@ -209,6 +213,7 @@ struct rrt_ctx {
   bool timed = false;
   uint32_t last_grid = 0;
   uint32_t last_heavy = 0;  // the last launch's heavy-list capacity (0: no heavy path)
+  uint32_t last_cont = 0;   // the last launch's continuation capacity (0: none)
   std::string last_kernel;
 };
 
@@ -307,6 +312,7 @@ void rrt_destroy(rrt_ctx* c) {
     hipFree(c->d_heavy_list);
     hipFree(c->d_strip_list);
     hipFree(c->d_audit);
+    hipFree(c->d_cont);
     hipFree(c->d_path_stack);
     for (uint32_t i = 0; i < rrt_ctx::kRing; ++i) {
       if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
@@ -1688,6 +1694,37 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         const uint32_t nv = (p->variant >> 16) & 0xfu;
         const double near = nv == 1 ? 0.0 : nv == 2 ? 1.1 : nv == 3 ? 1.5 : nv == 4 ? 2.0 : nv == 5 ? 3.0 : nv == 6 ? 5.0 : RRT_HEAVY_NEAR;
         kp.heavy_r2 = (near * c->hole.r) * (near * c->hole.r);
+        // Continuations (rrt_sample.hip cont_push): pixels of three or more adaptive
+        // steps (cfg4, 256 spp: its 8-way split ends on a few 8-step pixels, one step a round on
+        // the group path) go to waiting heavy blocks after a check with two or more steps to go.
+        // A/B in the environment: RRT_AB_CONT=0 off; RRT_AB_CONT_MIN=samples left;
+        // RRT_AB_CONT_ROOM=batch blocks of room
+        const char* ce = std::getenv("RRT_AB_CONT");
+        const bool cont_on = !(ce && ce[0] == '0') && p->ns_aa >= 3u * p->samples_per_batch;
+        if (cont_on) {
+          const uint32_t ccap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
+          if (c->cont_cap < ccap) {
+            hipFree(c->d_cont); c->d_cont = nullptr;
+            HIPCHK(c, hipMalloc(&c->d_cont, sizeof(ContRec) * ccap));
+            HIPCHK(c, hipMemset(c->d_cont, 0, sizeof(ContRec) * ccap));
+            c->cont_cap = ccap;
+          }
+          kp.cont = c->d_cont;
+          kp.cont_ctl = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);
+          kp.cont_cap = (uint32_t)c->cont_cap;
+          const char* cm = std::getenv("RRT_AB_CONT_MIN");
+          kp.cont_min_left = cm ? (uint32_t)std::strtoul(cm, nullptr, 10) : 2u * p->samples_per_batch;
+          if (++c->cont_seq == 0) c->cont_seq = 1;
+          kp.cont_seq = c->cont_seq;
+          const char* cr = std::getenv("RRT_AB_CONT_ROOM");
+          // launches of at most 60% of the frame (a rank's tiles): room for 32 heavy blocks from the
+          // start; a whole frame: none (its claim queue runs most of the launch, the heavy blocks
+          // start as batch blocks leave)
+          kp.cont_room = cr ? (uint32_t)std::strtoul(cr, nullptr, 10) : ((uint64_t)kp.n_pixels * 5u <= frame_px * 3u ? 32u : 0u);
+          kp.cont_ticks = 5000000u;  // 50 ms of wall clock (100 MHz)
+          const char* cw = std::getenv("RRT_AB_CONT_WAITERS");
+          kp.cont_waiters = cw ? (uint32_t)std::strtoul(cw, nullptr, 10) : ~0u;
+        }
       }
     }
   }
@@ -1785,7 +1822,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // the heavy pixels' kernel (batch launches with a heavy list): its waves per pixel and grid, and
   // whether the batch kernel sizes its room for it on the device (variant bits 22 / 23: A/B)
   const uint32_t hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
-  const int heavy_nw = nwv == 0 ? 2 : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;  // waves per heavy pixel
+  // waves per heavy pixel: 2 (a 64-sample pixel's two steps in one round), 4 with continuations
+  // (up to 256 slots: the remaining steps of a 256-sample pixel)
+  const int heavy_nw = nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;
   // heavy waves: hgv x the CU count (default 2), in blocks of heavy_nw waves
   const uint32_t heavy_waves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
   const uint32_t heavy_grid = std::max<uint32_t>(1u, heavy_waves / (uint32_t)heavy_nw);
@@ -1796,6 +1835,32 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     kp.heavy_grid = heavy_grid;
     kp.heavy_nw = (uint32_t)heavy_nw;
   }
+  // the batch kernel's waves/SIMD and grid (known before the upload: the heavy kernel's
+  // continuation wait ends when all kp.batch_waves batch waves have exited)
+  // waves/SIMD: the area-light build at 4 (cfg3 15.71 -> 15.33 ms, cfg2 10.33 -> 10.01 ms against
+  // 5, since the search tree took the local oversized leaves), the point-light build at 5 (cfg4
+  // 14.15 ms against 14.65 at 4) -- profiles/r03_heavy_ab.md
+  const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 4;
+  // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
+  const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
+  const int batch_w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 5) : gw;
+  uint32_t bgrid = grid;
+  if (batch && kp.heavy_list) {
+    // the batch grid leaves room for the heavy kernel's blocks (one per CU at most, <= 128 VGPRs
+    // and 25 KB of LDS next to four batch blocks), whichever kernel the hardware dispatches first
+    const uint32_t resident = (uint32_t)c->n_cu * (uint32_t)batch_w;  // blocks of 4 waves
+    const uint32_t spare = (static_room ? ((p->variant >> 12) & 0xfu) - 1u : 0u) * (uint32_t)c->n_cu +
+                           (heavy_waves + 3u) / 4u;  // room, in batch blocks
+    if (static_room) {
+      if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
+    } else if (!no_room) {
+      // room sized on the device to the heavy pixels the pass found (rrt_batch_kernel prologue,
+      // kp.heavy_grid / heavy_nw): the grid is exactly the resident blocks, so a block that
+      // leaves frees a slot no pending batch block can take
+      bgrid = std::min(bgrid, resident);
+    }
+  }
+  kp.batch_waves = bgrid * 4u;
   // tail priority threshold (A/B: RRT_AB_PRIO_TICKS in the environment)
   kp.prio_ticks = 50000u;
   if (const char* pt = std::getenv("RRT_AB_PRIO_TICKS")) kp.prio_ticks = (uint32_t)std::strtoul(pt, nullptr, 10);
@@ -1805,13 +1870,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   const char* tf[2] = {"false", "true"};
   char name[96];
   if (batch) {
-    // waves/SIMD: the area-light build at 4 (cfg3 15.71 -> 15.33 ms, cfg2 10.33 -> 10.01 ms against
-    // 5, since the search tree took the local oversized leaves), the point-light build at 5 (cfg4
-    // 14.15 ms against 14.65 at 4) -- profiles/r03_heavy_ab.md
-    const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 4;
-    // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
-    const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
-    const int w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 5) : gw;
+    const int w = batch_w;
     char first[32] = "";
     const uint32_t fwv = (p->variant >> 8) & 0xfu;  // pre-pass waves/SIMD (A/B), default 3
     const int fw = (lean == 1 && (fwv == 4 || fwv == 5)) ? (int)fwv : 3;
@@ -1823,38 +1882,24 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
                                  stream));
     if (kp.claim_list) HIPCHK(c, rrt_launch_pixel_proof(c->d_kp, kp.n_pixels, kp.strip_list != nullptr, stream));
     HIPCHK(c, hipEventRecord(c->ev_main[ring], stream));
-    uint32_t bgrid = grid;
+    const uint32_t hwv = (p->variant >> 24) & 0xfu;
+    const int hw = hwv == 5 ? 5 : 4;  // the heavy kernel's waves/SIMD budget
     if (kp.heavy_list) {
       // the heavy pixels' kernel (rrt_sample.hip rrt_heavy_kernel) on the side stream (its own
-      // hardware queue), after the pass, beside the batch kernel; the batch grid leaves room for
-      // its blocks (one per CU at most, <= 128 VGPRs and 23 KB of LDS next to four batch blocks),
-      // whichever kernel the hardware dispatches first
-      const uint32_t hwv = (p->variant >> 24) & 0xfu;
-      const int hw = hwv == 5 ? 5 : 4;
-      const int nw = heavy_nw;
-      const uint32_t hgrid = heavy_grid;
-      const uint32_t resident = (uint32_t)c->n_cu * (uint32_t)(lean == 1 || lean == 2 ? w : gw);  // blocks of 4 waves
-      const uint32_t spare = (static_room ? ((p->variant >> 12) & 0xfu) - 1u : 0u) * (uint32_t)c->n_cu +
-                             (heavy_waves + 3u) / 4u;  // room, in batch blocks
-      if (static_room) {
-        if (!no_room && bgrid + spare > resident) bgrid = resident > spare ? resident - spare : 1u;
-      } else if (!no_room) {
-        // room sized on the device to the heavy pixels the pass found (rrt_batch_kernel prologue,
-        // kp.heavy_grid / heavy_nw): the grid is exactly the resident blocks, so a block that
-        // leaves frees a slot no pending batch block can take
-        bgrid = std::min(bgrid, resident);
-      }
+      // hardware queue), after the pass, beside the batch kernel
       HIPCHK(c, hipEventRecord(c->ev_go, stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
       join_guard.state = 1;
-      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, nw, hgrid, c->side));
+      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, heavy_grid, 0, c->side));
       HIPCHK(c, hipEventRecord(c->ev_heavy, c->side));
       join_guard.state = 2;
     }
-    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, lean == 1 || lean == 2 ? w : gw, bgrid, stream));
+    HIPCHK(c, rrt_launch_batch(kp, c->d_kp, lean, w, bgrid, stream));
     if (kp.heavy_list) {
       HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
       join_guard.state = 3;
+      // continuations no heavy block took (it stopped waiting first): rendered behind both kernels
+      if (kp.cont) HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, 16u, 1, stream));
     }
   } else if (path_pool) {
     std::snprintf(name, sizeof(name), "%srrt_path_kernel<%d>", deep_list ? "rrt_pixel_proof_kernel + " : "",
@@ -1877,6 +1922,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   }
   c->last_kernel = name;
   c->last_heavy = kp.heavy_list ? kp.heavy_cap : 0u;
+  c->last_cont = kp.cont ? kp.cont_cap : 0u;
   HIPCHK(c, hipEventRecord(c->ev1[ring], stream));
 #if RRT_PROFILE
   if (wd_ms > 0) {
@@ -2060,6 +2106,12 @@ extern "C" int rrt_get_stats(const rrt_ctx* cc, rrt_stats* out) {
     uint32_t n = 0;
     if (hipMemcpy(&n, c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1), sizeof(n), hipMemcpyDeviceToHost) == hipSuccess)
       out->last_heavy_pixels = std::min<uint32_t>(n, c->last_heavy);
+  }
+  if (c->device >= 0 && c->timed && c->last_cont) {  // continuation records reserved (capped)
+    uint32_t n = 0;
+    if (hipMemcpy(&n, c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2 + RRT_CONT_TAIL), sizeof(n),
+                  hipMemcpyDeviceToHost) == hipSuccess)
+      out->last_cont_pixels = std::min<uint32_t>(n, c->last_cont);
   }
   return RRT_OK;
 }

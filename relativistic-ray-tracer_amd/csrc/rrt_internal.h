@@ -173,6 +173,20 @@ __host__ __device__ __forceinline__ uint32_t claim_r(uint32_t c, uint32_t ts) {
 #define RRT_MAX_QUEUES 8
 #define RRT_QUEUE_STRIDE 16  // counters 64 B apart
 
+// A pixel handed from rrt_batch_kernel to rrt_heavy_kernel between two adaptive steps (a
+// continuation): its position, the samples folded so far and their sums in the
+// reference's accumulation types (raytrace_pixel, part1_code.cpp:136-158), and the next sample's
+// draw offset.  seq = the launch's KParams::cont_seq once the record is written.
+struct ContRec {
+  double s1, s2;
+  float r, g, b;
+  uint32_t x, y, slot, i, O;
+  uint32_t seq, pad[3];
+};
+// KParams::cont_ctl words (RRT_QUEUE_STRIDE apart): records reserved, records taken, heavy blocks
+// waiting for one, batch waves exited
+enum { RRT_CONT_TAIL = 0, RRT_CONT_HEAD = 1, RRT_CONT_IDLE = 2, RRT_CONT_EXITED = 3, RRT_CONT_WORDS = 4 };
+
 struct KParams {
   // scene
   const DNode* nodes;
@@ -272,6 +286,19 @@ struct KParams {
   // [2 k + 1] violations per proof k (RRT_AUDIT_*); null: no audit
   unsigned long long* audit;  // 64-bit: a 1080p frame audited at every_log2 = 0 exceeds 2^32 checks
   uint32_t audit_shift, audit_pad;
+  // continuations: a batch-kernel group whose pixel still has >= cont_min_left
+  // samples to go after an adaptive check hands it to a heavy block that is waiting for work
+  // (cont_ctl[RRT_CONT_IDLE] > 0), which renders the remaining steps' draw-offset slots in parallel.
+  // cont null: off.  The heavy blocks stop waiting once batch_waves batch waves have exited.
+  ContRec* cont;
+  uint32_t* cont_ctl;
+  uint32_t cont_cap, cont_min_left;
+  uint32_t cont_seq, batch_waves;
+  uint32_t cont_room;     // batch blocks that leave at once, room for the waiting heavy blocks
+  uint32_t cont_ticks;    // a heavy block stops waiting after this long without work (wall clock)
+  uint32_t cont_waiters;  // heavy blocks blockIdx < cont_waiters wait for continuations; the others
+                          // leave once the heavy list is done (their slots go back to the batch kernel)
+  uint32_t cont_pad;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

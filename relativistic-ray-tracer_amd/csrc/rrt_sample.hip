@@ -406,29 +406,53 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
 // on the first heavy pixel of bunny_B1_160x120_s16 while the out-of-line build rendered it
 // bit-exactly (tools/probe_case.py; cause not found); called out of line from the batch kernel,
 // it doubled the group loop's spills (cfg3 batch kernel 17.3 -> 33.5 ms), hence its own kernel.
+// The same block also takes continuations (ContRec, from the batch kernel): a pixel some of whose
+// steps are already folded, resumed from its sums and draw offset.
 template <int NW>
 struct HeavyLds {
   rrt::ShadeLdsN<64 * NW> sh;  // parked hit records (direct_importance_parked)
   float r[64 * NW], g[64 * NW], b[64 * NW];  // each slot's sample radiance
   uint64_t hits[NW];  // each wave's ballot of hits
-  uint32_t hx;        // the claimed heavy-list entry
+  // the claimed pixel (thread 0 writes it between block barriers): position, output slot, samples
+  // folded, first slot (draw offset / Dm) and the sums so far
+  double s1, s2;
+  float r0, g0, b0;
+  uint32_t x, y, slot, i, m0;
+  uint32_t go;
 };
+// Thread 0: the pixel proof pass's heavy-list entry k as a fresh pixel
+template <int NW>
+__device__ __forceinline__ void heavy_take_listed(const KParams& kp, HeavyLds<NW>& hl, uint32_t k) {
+  const uint32_t ts = kp.tile_size, tpix = ts * ts;
+  const uint32_t ix = kp.heavy_list[k];
+  const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
+  hl.x = kp.tiles[2 * tl] + r % ts; hl.y = kp.tiles[2 * tl + 1] + r / ts; hl.slot = tl * tpix + r;
+  hl.i = 0; hl.m0 = 0; hl.r0 = 0.0f; hl.g0 = 0.0f; hl.b0 = 0.0f; hl.s1 = 0.0; hl.s2 = 0.0;
+}
+// Thread 0: continuation record h once its writer has published it (seq), as the pixel to resume
+template <int NW>
+__device__ __forceinline__ void heavy_take_cont(const KParams& kp, HeavyLds<NW>& hl, uint32_t h) {
+  ContRec* rc = kp.cont + h;
+  while (__hip_atomic_load(&rc->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != kp.cont_seq)
+    __builtin_amdgcn_s_sleep(2);  // reserved by a running batch wave, whose stores are on their way
+  hl.x = rc->x; hl.y = rc->y; hl.slot = rc->slot; hl.i = rc->i; hl.m0 = rc->O / kp.draws_miss;
+  hl.r0 = rc->r; hl.g0 = rc->g; hl.b0 = rc->b; hl.s1 = rc->s1; hl.s2 = rc->s2;
+}
 template <int LEAN, int W, int NW>
-__device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& hl, uint32_t t, uint32_t hx,
-                                               rrt::Counters& cn) {
+__device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& hl, uint32_t t, rrt::Counters& cn) {
   using namespace rrt;
   constexpr uint32_t NS = 64u * NW;  // slots per round
-  const uint32_t ts = kp.tile_size, tpix = ts * ts;
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit, S1 = Dh / Dm;
   const DCamera& cam = kp.cam;
-  const uint32_t ix = kp.heavy_list[hx];
-  const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
-  const uint32_t x = kp.tiles[2 * tl] + r % ts, y = kp.tiles[2 * tl + 1] + r / ts;
+  const uint32_t x = hl.x, y = hl.y, slot = hl.slot;
   const uint64_t key = rrt_pixel_key(kp.seed, x, y);
-  spec ret = S(0, 0, 0);
-  double s1 = 0.0, s2 = 0.0;
-  uint32_t i = 0, m0 = 0;  // samples folded; the round's first slot
+  spec ret = S(hl.r0, hl.g0, hl.b0);
+  double s1 = hl.s1, s2 = hl.s2;
+  uint32_t i = hl.i, m0 = hl.m0;  // samples folded; the round's first slot
   for (;;) {
+    // the chain of the ns_aa - i samples left spans at most S1 (ns_aa - i) slots: lanes beyond
+    // that are never reached by the fold and stay idle
+    const uint32_t lim = S1 * (kp.ns_aa - i);
     const uint32_t sl = m0 + t;
     Rng g; g.key = key; g.ctr = sl * Dm;
     double jx, jy; g.grid(jx, jy);  // Camera::generate_ray (part1_code.cpp:182-187) at the slot's jitter
@@ -438,7 +462,7 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     const v3 wd = unit(w);
     Isect is;
-    const bool hit = !camera_proven_miss<false, false>(kp, ld3(cam.pos), wd, cn) &&
+    const bool hit = t < lim && !camera_proven_miss<false, false>(kp, ld3(cam.pos), wd, cn) &&
                      query_nx<false, false, false>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (hit) {
@@ -477,7 +501,6 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
     if (st) break;
   }
   if (t == 0) {
-    const uint32_t slot = tl * tpix + r;
     const spec rr = ret / (float)i;
     kp.rgb[3 * slot] = rr.r; kp.rgb[3 * slot + 1] = rr.g; kp.rgb[3 * slot + 2] = rr.b;
     kp.count[slot] = (int32_t)i;
@@ -488,44 +511,94 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
 // The heavy pixels' kernel (heavy pixels), launched after the pixel proof pass on
 // the context's high-priority side stream, beside the batch kernel, which leaves room for its
 // blocks (rrt_host.cpp): each block of NW waves takes heavy pixels one at a time, at issue
-// priority 3.
+// priority 3 -- first the pass's heavy list, then (kp.cont) continuations from the batch kernel:
+// a block with nothing to do counts itself idle (cont_ctl[RRT_CONT_IDLE], which lets the batch
+// kernel's groups hand pixels over) and takes the next published record.  It never depends on the
+// batch kernel to finish: it stops waiting once every batch wave has exited or after cont_ticks
+// without a record, and drain (a launch behind both kernels on the main stream) renders whatever
+// records are left untaken, so an ordering of the two kernels that the hardware chooses cannot
+// hang the launch or drop a pixel.
 template <int LEAN, int HW, int NW>
-__global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp) {
+__global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp, int drain) {
   const KParams& kp = *kpp;
   using namespace rrt;
   __shared__ HeavyLds<NW> hl;
   const uint32_t t = threadIdx.x;
   Counters cn = {};
-  const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
+  const uint32_t nh = drain ? 0u : min(*kp.heavy_count, kp.heavy_cap);
+  uint32_t* const cc = kp.cont_ctl;
+  bool listed = !drain, idle = false;  // (thread 0's)
   __builtin_amdgcn_s_setprio(3);
 #if RRT_PROFILE
   volatile uint32_t* wd = kp.wd ? kp.wd + RRT_WD_HEAVY + 4u * (blockIdx.x & 0x7fffu) : nullptr;
   uint32_t wd_it = 0;
 #endif
   for (;;) {
-    if (t == 0) hl.hx = atomicAdd(kp.heavy_count + 1, 1u);
+    if (t == 0) {
+      uint32_t go = 0;
+      if (listed) {
+        const uint32_t k = atomicAdd(kp.heavy_count + 1, 1u);
+        if (k < nh) { heavy_take_listed(kp, hl, k); go = 1; }
+        else listed = false;
+      }
+      if (!go && kp.cont && drain) {  // behind both kernels: every reserved record is written
+        const uint32_t h = atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, 1u);
+        if (h < min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap)) {
+          heavy_take_cont(kp, hl, h);
+          go = 1;
+        }
+      } else if (!go && kp.cont && blockIdx.x < kp.cont_waiters) {
+        if (!idle) { atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u); idle = true; }
+        uint64_t since = wall_clock64();
+        for (;;) {
+          const uint32_t hd = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t tl = min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap);
+          if (hd < tl) {
+            uint32_t e = hd;
+            if (__hip_atomic_compare_exchange_strong(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, &e, hd + 1u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              atomicSub(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
+              idle = false;
+              heavy_take_cont(kp, hl, hd);
+              go = 1;
+              break;
+            }
+            continue;
+          }
+          // the batch kernel is done (its waves have published every record they reserved), or
+          // nothing has come for cont_ticks: stop waiting
+          const bool fin = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_EXITED, __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_AGENT) >= kp.batch_waves;
+          if (fin && hd < min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap))
+            continue;  // published before the last wave left
+          if (fin || wall_clock64() - since > kp.cont_ticks) {
+            atomicSub(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
+            idle = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(16);
+        }
+      }
+      hl.go = go;
+    }
     __syncthreads();
-    const uint32_t k = hl.hx;
-    __syncthreads();  // every thread has read it before thread 0 claims again
+    const uint32_t go = hl.go;
+    __syncthreads();  // every thread has read the claim before thread 0 claims again
 #if RRT_PROFILE
-    if (wd && t == 0) { wd[0] = ++wd_it; wd[1] = nh; wd[2] = k; wd[3] = 0x11u; }
+    if (wd && t == 0) { wd[0] = ++wd_it; wd[1] = nh; wd[2] = hl.slot; wd[3] = 0x11u; }
 #endif
-    if (k >= nh) break;
+    if (!go) break;
 #if RRT_PROFILE
     const uint64_t w_h = wall_clock64();
+    const uint32_t pslot = hl.slot;
 #endif
-    heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl, t, k, cn);
+    heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl, t, cn);
 #if RRT_PROFILE
     if (wd && t == 0) wd[3] = 0x12u;  // pixel done
-#endif
-#if RRT_PROFILE  // elapsed ticks; "rounds" 1
-    if (t == 0) {
-      const uint32_t ts = kp.tile_size, tpix = ts * ts;
-      const uint32_t ix = kp.heavy_list[k], tl = kp.tile_order[ix / tpix], slot = tl * tpix + claim_r(ix % tpix, ts);
-      if (slot < (1u << 21)) {
-        rrt_prof_px[slot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
-        rrt_prof_px_end[slot] = (uint32_t)wall_clock64();
-      }
+    if (t == 0 && pslot < (1u << 21)) {  // elapsed ticks; "rounds" 1
+      rrt_prof_px[pslot] = ((uint32_t)min(wall_clock64() - w_h, (uint64_t)0xffffff) << 8) | 1u;
+      rrt_prof_px_end[pslot] = (uint32_t)wall_clock64();
     }
 #endif
   }
@@ -534,9 +607,10 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
 #endif
 }
 
-// waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks
-hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, hipStream_t stream) {
-#define RRT_LAUNCH_H(L, W, N) hipLaunchKernelGGL((rrt_heavy_kernel<L, W, N>), dim3(grid), dim3(64 * N), 0, stream, d_kp)
+// waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks; drain: the launch behind
+// the batch and heavy kernels that renders untaken continuation records
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, int drain, hipStream_t stream) {
+#define RRT_LAUNCH_H(L, W, N) hipLaunchKernelGGL((rrt_heavy_kernel<L, W, N>), dim3(grid), dim3(64 * N), 0, stream, d_kp, drain)
   if (lean == 1) {
     if (waves == 5) {
       if (nw == 1) RRT_LAUNCH_H(1, 5, 1); else if (nw == 4) RRT_LAUNCH_H(1, 5, 4); else RRT_LAUNCH_H(1, 5, 2);
@@ -550,6 +624,33 @@ hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, ui
   }
 #undef RRT_LAUNCH_H
   return hipGetLastError();
+}
+
+// Continuations.  A group leader whose pixel did not stop at an adaptive check and
+// has at least kp.cont_min_left samples to go hands it to a heavy block when one is waiting for
+// work and no record already waits for it: it reserves record k, writes the pixel's state there and
+// publishes it (seq, release).  The heavy block resumes the fold from that state with its 64 NW
+// slots per round, so the result is the one the group would have reached.  false: keep the pixel.
+__device__ __forceinline__ bool cont_push(const KParams& kp, uint32_t x, uint32_t y, uint32_t slot, uint32_t i,
+                                          uint32_t O, rrt::spec ret, double s1, double s2) {
+  uint32_t* const cc = kp.cont_ctl;
+  const uint32_t idle = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (idle == 0) return false;
+  const uint32_t tl = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t hd = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int32_t)(tl - hd) >= (int32_t)idle || tl >= kp.cont_cap) return false;
+  const uint32_t k = atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, 1u);
+  if (k >= kp.cont_cap) return false;
+  ContRec* rc = kp.cont + k;
+  rc->s1 = s1; rc->s2 = s2; rc->r = ret.r; rc->g = ret.g; rc->b = ret.b;
+  rc->x = x; rc->y = y; rc->slot = slot; rc->i = i; rc->O = O;
+  __hip_atomic_store(&rc->seq, kp.cont_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+// a batch wave leaves: once all have, the heavy blocks stop waiting for continuations
+__device__ __forceinline__ void cont_wave_exit(const KParams& kp, uint32_t lane) {
+  if (kp.cont && lane == 0)
+    __hip_atomic_fetch_add(kp.cont_ctl + RRT_QUEUE_STRIDE * RRT_CONT_EXITED, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int LEAN, int WAVES>
@@ -586,10 +687,14 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
   // need, in batch blocks of 4 waves -- leave at once, so the heavy kernel's blocks take their
   // slots whichever kernel the hardware dispatched first.  A launch with no heavy pixels keeps
   // every block (the heavy kernel's blocks then start at its end and find the list empty).
+  // With continuations the heavy blocks wait for work the whole launch: kp.cont_room blocks at least.
   if (kp.heavy_grid) {
     const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
-    const uint32_t need = (min(nh, kp.heavy_grid) * kp.heavy_nw + 3u) / 4u;
-    if (blockIdx.x + min(need, gridDim.x - 1u) >= gridDim.x) return;
+    const uint32_t need = max((min(nh, kp.heavy_grid) * kp.heavy_nw + 3u) / 4u, kp.cont_room);
+    if (blockIdx.x + min(need, gridDim.x - 1u) >= gridDim.x) {
+      cont_wave_exit(kp, lane);
+      return;
+    }
   }
   bool have = false, done = false;
   uint32_t q = blockIdx.x % kp.n_queues, q_left = kp.n_queues;  // claim queue (group leaders)
@@ -931,7 +1036,10 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         if (1.96 * sd / sqrt((double)i) <= (double)kp.max_tolerance * avg) st = true;
       }
       if (st) stop = 1;
-      if (stop) {
+      else if (kp.cont && (uint32_t)((int)kp.ns_aa - i) >= kp.cont_min_left &&
+               cont_push(kp, lget(gs.px, gid), lget(gs.py, gid), lget(gs.slot, gid), (uint32_t)i, O, ret, s1, s2))
+        stop = 2;  // handed over: the heavy block writes the result
+      if (stop == 1) {
         const uint32_t slot = lget(gs.slot, gid);
 #if RRT_PROFILE
         {  // elapsed wall ticks (26 bits) | rounds (7) | steps (7) | pixel slot (24)
@@ -949,7 +1057,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
         kp.rgb[3 * slot] = r.r; kp.rgb[3 * slot + 1] = r.g; kp.rgb[3 * slot + 2] = r.b;
         kp.count[slot] = i;
         if (kp.draws) kp.draws[slot] = O;
-      } else {
+      } else if (stop == 0) {
         lput(gs.rr, gid, ret.r); lput(gs.rg, gid, ret.g); lput(gs.rb, gid, ret.b);
         lput(gs.s1, gid, s1); lput(gs.s2, gid, s2);
         lput(gs.i, gid, (uint32_t)i); lput(gs.O, gid, O); lput(gs.hyp, gid, hyp);
@@ -959,6 +1067,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     if (stop) have = false;
     RRT_ACC(t_fold, tf0);
   }
+  cont_wave_exit(kp, lane);
 #if RRT_PROFILE
   if (wd && lane == 0) wd[3] = 0xdeadu;  // exited
 #endif

@@ -95,7 +95,7 @@ class Stats(C.Structure):
                 ("n_clean", C.c_uint32), ("n_big", C.c_uint32),
                 ("grid_free_frac", C.c_float), ("last_kernel_ms", C.c_float), ("grid_blocks", C.c_uint32),
                 ("block_threads", C.c_uint32), ("kernel", C.c_char * 64), ("last_main_kernel_ms", C.c_float),
-                ("last_heavy_pixels", C.c_uint32)]
+                ("last_heavy_pixels", C.c_uint32), ("last_cont_pixels", C.c_uint32)]
 
 
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)

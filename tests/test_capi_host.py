@@ -22,7 +22,7 @@ def test_exports_match_header():
     L = rrt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rrt_abi_version() == 4
+    assert L.rrt_abi_version() == 5
 
 
 def test_proof_audit_needs_a_device():

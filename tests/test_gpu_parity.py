@@ -260,3 +260,93 @@ def test_two_streams_one_context(gpu):
         frames.append(fr[c.y0:c.y0 + c.h, c.x0:c.x0 + c.w])
     assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
     assert np.array_equal(frames[0].view(np.uint32), c.px["rgb"].view(np.uint32))
+
+
+# Continuations: pixels of >= 3 adaptive steps that have not stopped at a check are
+# handed from the batch kernel to waiting heavy blocks.  Modes: the library default; "eager" hands
+# over every pixel that did not stop (RRT_AB_CONT_MIN=1) with room for 64 heavy blocks from the
+# launch's start; "off" (RRT_AB_CONT=0).  Read by the library at every launch.
+CONT_MODES = {"default": {}, "eager": {"RRT_AB_CONT_MIN": "1", "RRT_AB_CONT_ROOM": "64"}, "off": {"RRT_AB_CONT": "0"}}
+CONT_CASES = ["cfg4_knot_4k_s256_crop", "cfg4_knot_4k_s256_crop2", "cfg4_knot_4k_s256_crop3", "spheres_96x72_s64_a16"]
+
+
+@pytest.fixture
+def cont_env():
+    keys = {k for m in CONT_MODES.values() for k in m}
+    saved = {k: os.environ.get(k) for k in keys}
+
+    def set_mode(mode):
+        for k in keys:
+            os.environ.pop(k, None)
+        os.environ.update(CONT_MODES[mode])
+
+    yield set_mode
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+@pytest.mark.parametrize("mode", sorted(CONT_MODES))
+@pytest.mark.parametrize("name", CONT_CASES)
+def test_continuations(gpu, cont_env, name, mode):
+    """Bit-exact with the batch kernel's pixels resumed by the heavy kernel from their folded sums."""
+    cont_env(mode)
+    c = Case(name)
+    rgb, cnt, draws, _ = render(gpu, c)
+    st = gpu.stats()
+    print(name, mode, "continuations", st.last_cont_pixels, "heavy", st.last_heavy_pixels, st.kernel.decode())
+    check(c, rgb, cnt, draws)
+    if mode == "off":
+        assert st.last_cont_pixels == 0
+    if mode == "eager":  # some pixel of each case goes past its first check
+        assert st.last_cont_pixels > 0
+
+
+@pytest.mark.parametrize("world", [8])
+def test_rank_tiles_cfg4_crops(gpu, cont_env, world):
+    """cfg4 (4K, 256 spp) split `world` ways as bench.py splits it: every rank's tiles that cover
+    the three reference-rendered crops, rendered through the device path (heavy pixels and
+    continuations on: a rank's launch is a small part of the frame), unpacked into one frame:
+    bit-exact against the reference's crops."""
+    torch = pytest.importorskip("torch")
+    cont_env("default")
+    cases = [Case(n) for n in CONT_CASES[:3]]
+    c = cases[0]
+    gpu.set_scene(rrt.SceneFile(c.scene_path))
+    gpu.set_envmap(c.envmap)
+    gpu.set_camera(rrt.load_camera(c.camera_path))
+    bh = c.cfg["bh"]
+    gpu.set_black_hole(bh[:3], bh[3], bh[4])
+    W, H, ts, g = c.frame_w, c.frame_h, 32, c.cfg
+    p = rrt.render_params(W, H, ns_aa=g["ns_aa"], max_ray_depth=g["max_ray_depth"], ns_area_light=g["ns_area_light"],
+                          samples_per_batch=g["samples_per_batch"], max_tolerance=g["max_tolerance"])
+    out_rgb = torch.full((H * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+    out_cnt = torch.full((H * W,), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def covers(x, y):
+        return any(x < k.x0 + k.w and x + ts > k.x0 and y < k.y0 + k.h and y + ts > k.y0 for k in cases)
+
+    n_cont = 0
+    for r in range(world):
+        tiles = np.array([t for t in rrt.partition_tiles(W, H, ts, r, world) if covers(int(t[0]), int(t[1]))],
+                         np.uint32).reshape(-1, 2)
+        if len(tiles) == 0:
+            continue
+        prgb = torch.zeros(len(tiles) * ts * ts * 3, dtype=torch.float32, device="cuda")
+        pcnt = torch.zeros(len(tiles) * ts * ts, dtype=torch.int32, device="cuda")
+        gpu.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        n_cont += gpu.stats().last_cont_pixels
+        gpu.unpack_tiles_device(tiles, ts, W, H, prgb.data_ptr(), pcnt.data_ptr(), out_rgb.data_ptr(),
+                                out_cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    rgb = out_rgb.cpu().numpy().reshape(H, W, 3)
+    cnt = out_cnt.cpu().numpy().reshape(H, W)
+    print("world", world, "continuations", n_cont)
+    for k in cases:
+        ys, xs = slice(k.y0, k.y0 + k.h), slice(k.x0, k.x0 + k.w)
+        assert np.array_equal(rgb[ys, xs].view(np.uint32), k.px["rgb"].view(np.uint32)), k.name
+        assert np.array_equal(cnt[ys, xs], k.px["count"]), k.name
