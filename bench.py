@@ -131,7 +131,7 @@ FP64_CYCLES_PER_WAVE_INST = 4.0
 N_SIMD = 1024
 
 
-PROFILE_ROUNDS = ("r05", "r04", "r03")  # profiles/ files searched, newest first (each must match the build)
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03")  # profiles/ files searched, newest first (each must match the build)
 
 
 def find_profile(explicit, names, workload, kernel):

@@ -309,6 +309,10 @@ void rrt_group_destroy(rrt_group* g);
  * tiles_out and returns the number of tiles (or a negative error). */
 int rrt_partition_tiles(uint32_t frame_w, uint32_t frame_h, uint32_t tile_size, uint32_t rank, uint32_t world,
                         uint32_t* tiles_out, uint32_t max_tiles);
+/* The same deal over the tiles of a region (x0, y0, w x h pixels; tiles from its origin): the split
+ * rrt_group_render uses for its members.  rrt_partition_tiles is the region (0, 0, frame). */
+int rrt_region_tiles(uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t tile_size, uint32_t rank,
+                     uint32_t world, uint32_t* tiles_out, uint32_t max_tiles);
 
 /* ---------------------------------------------------------------- introspection */
 typedef struct {

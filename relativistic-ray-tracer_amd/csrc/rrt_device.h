@@ -1641,27 +1641,18 @@ __device__ __forceinline__ spec emission(const DBsdf& b) {
   return b.type == B_EMISSION ? S(b.p[0], b.p[1], b.p[2]) : S(0, 0, 0);
 }
 __device__ __forceinline__ double clamp_b(double n, double lo, double hi) { return std_max(lo, std_min(n, hi)); }
-// The microfacet BSDF's exp/log/erf/atan/tan (bsdf.cpp:45-96, bsdf.h:159-191).  rrt_glibm.h restates
-// glibc's (bit-exact against the library on the CPU and, through rrt_libm_eval, on the GPU), but
-// compiled into the general kernel builds (RRT_MF_GLIBM 1) they made those builds fault
-// intermittently on scenes without a microfacet BSDF (cause not found), so the
-// kernels call the device libm here and the microfacet goldens are held to the north-star bound.
-#ifndef RRT_MF_GLIBM
-#define RRT_MF_GLIBM 0
-#endif
-#if RRT_MF_GLIBM
+// The microfacet BSDF's exp/log/erf/atan/tan (bsdf.cpp:45-96, bsdf.h:159-191): glibc's own,
+// restated in rrt_glibm.h (bit-exact against the library on the CPU and, through rrt_libm_eval, on
+// the GPU), so the microfacet scenes are bit-exact too.  (Round 5 had to keep the device libm here:
+// with the restatements inlined into bsdf_f the inliner stopped inlining the direct-lighting
+// functions, and the general kernels' out-of-line calls to them faulted -- DESIGN.md §3.  Those
+// functions are __forceinline__ now, so every build has the same call structure with or without
+// the restatements.)
 #define RRT_MF_TAN rrt_glibm_tan
 #define RRT_MF_ERF rrt_glibm_erf
 #define RRT_MF_EXP rrt_glibm_exp
 #define RRT_MF_ATAN rrt_glibm_atan
 #define RRT_MF_LOG rrt_glibm_log
-#else
-#define RRT_MF_TAN tan
-#define RRT_MF_ERF erf
-#define RRT_MF_EXP exp
-#define RRT_MF_ATAN atan
-#define RRT_MF_LOG log
-#endif
 __device__ __forceinline__ double mf_theta(v3 w) { return rrt_glibm_acos(clamp_b(w.z, -1.0 + 1e-5, 1.0 - 1e-5)); }
 __device__ __forceinline__ double mf_lambda(float alpha, v3 w) {
   double theta = mf_theta(w);
@@ -1705,7 +1696,7 @@ __device__ __forceinline__ bool refract(v3 wo, v3& wi, float ior) {  // bsdf.cpp
   if (wo.z > 0) wi.z = -wi.z;
   return true;
 }
-__device__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf, bool mf_hemi = false) {
+__device__ __forceinline__ spec bsdf_sample_f(const DBsdf& b, Rng& g, v3 wo, v3& wi, float& pdf, bool mf_hemi = false) {
   switch (b.type) {
     case B_DIFFUSE:
       wi = cosine_sample(g, &pdf);
@@ -1818,7 +1809,7 @@ __device__ __forceinline__ spec env_sample(const DEnv& e, Rng& g, v3& wi, float&
 // ------------------------------------------------------------------ lights (light.cpp)
 // LEAN: every light is an area or a point light
 template <int LEAN = 0>
-__device__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf,
+__device__ __forceinline__ spec light_sample_L(const DEnv& env, const DLight& l, Rng& g, v3 p, v3& wi, float& dist, float& pdf,
                                bool env_hemi = false) {
   spec rad = S(l.rad[0], l.rad[1], l.rad[2]);
   switch (LEAN == 1 ? 0u : LEAN == 2 ? (l.type == 1u ? 1u : 0u) : l.type) {

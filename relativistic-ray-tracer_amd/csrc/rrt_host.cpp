@@ -323,6 +323,7 @@ void rrt_destroy(rrt_ctx* c) {
     if (c->ev_go) hipEventDestroy(c->ev_go);
     if (c->ev_heavy) hipEventDestroy(c->ev_heavy);
     if (c->side) hipStreamDestroy(c->side);
+
     if (c->stream) hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1264,19 +1265,25 @@ extern "C" void rrt_kerr_frame(const double* axis, double* ex, double* ey, doubl
   ey[2] = ez[0] * ex[1] - ez[1] * ex[0];
 }
 
-extern "C" int rrt_partition_tiles(uint32_t fw, uint32_t fh, uint32_t ts, uint32_t rank, uint32_t world,
-                                   uint32_t* out, uint32_t max_tiles) {
+// The block-cyclic serpentine deal of a region's tiles (origin x0, y0; w x h pixels) over `world`
+// ranks: tile k of the serpentine order (rows alternate direction) goes to rank k % world.
+extern "C" int rrt_region_tiles(uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t ts, uint32_t rank,
+                                uint32_t world, uint32_t* out, uint32_t max_tiles) {
   if (ts == 0 || world == 0 || rank >= world) return RRT_E_INVALID;
-  uint32_t tw = (fw + ts - 1) / ts, th = (fh + ts - 1) / ts, n = 0, k = 0;
+  uint32_t tw = (w + ts - 1) / ts, th = (h + ts - 1) / ts, n = 0, k = 0;
   for (uint32_t ty = 0; ty < th; ++ty) {
     for (uint32_t i = 0; i < tw; ++i, ++k) {
       uint32_t tx = (ty & 1) ? (tw - 1 - i) : i;  // serpentine
       if (k % world != rank) continue;
-      if (out && n < max_tiles) { out[2 * n] = tx * ts; out[2 * n + 1] = ty * ts; }
+      if (out && n < max_tiles) { out[2 * n] = x0 + tx * ts; out[2 * n + 1] = y0 + ty * ts; }
       ++n;
     }
   }
   return (int)n;
+}
+extern "C" int rrt_partition_tiles(uint32_t fw, uint32_t fh, uint32_t ts, uint32_t rank, uint32_t world,
+                                   uint32_t* out, uint32_t max_tiles) {
+  return rrt_region_tiles(0, 0, fw, fh, ts, rank, world, out, max_tiles);
 }
 
 static int ensure(rrt_ctx* c, void** p, size_t& cap, size_t need, size_t elem) {
@@ -1341,12 +1348,12 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // into `stream` first (so the fence above covers its reads of d_kp / d_counter / the heavy list):
   // 1 = launched, 2 = its completion event recorded, 3 = joined
   struct JoinGuard {
-    rrt_ctx* c; hipStream_t s; int state;
+    rrt_ctx* c; hipStream_t s; hipStream_t fork; hipEvent_t done; int state;
     ~JoinGuard() {
-      if (state == 1) (void)hipStreamSynchronize(c->side);
-      else if (state == 2) (void)hipStreamWaitEvent(s, c->ev_heavy, 0);
+      if (state == 1) (void)hipStreamSynchronize(fork);
+      else if (state == 2) (void)hipStreamWaitEvent(s, done, 0);
     }
-  } join_guard{c, stream, 0};
+  } join_guard{c, stream, c->side, c->ev_heavy, 0};
   if (c->tiles_cap < n_tiles) {
     // hipFree waits for the device, so no launch still reads the old list
     hipFree(c->d_tiles); c->d_tiles = nullptr;
@@ -1690,17 +1697,21 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         kp.heavy_list = c->d_heavy_list;
         kp.heavy_count = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);
         kp.heavy_cap = cap;
+
         // A/B (variant bits 16..19): 1: capture-boundary pixels only, 2 .. 6: near 1.1 / 1.5 / 2.0 / 3.0 / 5.0
         const uint32_t nv = (p->variant >> 16) & 0xfu;
         const double near = nv == 1 ? 0.0 : nv == 2 ? 1.1 : nv == 3 ? 1.5 : nv == 4 ? 2.0 : nv == 5 ? 3.0 : nv == 6 ? 5.0 : RRT_HEAVY_NEAR;
         kp.heavy_r2 = (near * c->hole.r) * (near * c->hole.r);
-        // Continuations (rrt_sample.hip cont_push): pixels of three or more adaptive
-        // steps (cfg4, 256 spp: its 8-way split ends on a few 8-step pixels, one step a round on
-        // the group path) go to waiting heavy blocks after a check with two or more steps to go.
-        // A/B in the environment: RRT_AB_CONT=0 off; RRT_AB_CONT_MIN=samples left;
-        // RRT_AB_CONT_ROOM=batch blocks of room
+        // Continuations (rrt_sample.hip cont_push): in launches of at most 60% of the
+        // frame (a rank's share), pixels of three or more adaptive steps go to waiting heavy blocks
+        // after a check with two or more steps to go (cfg4, 256 spp: the 8-way split's ranks ended
+        // on a few 8-step pixels, one step a round on the group path; profiles/r06_cont_w8_cfg4.txt).
+        // A whole frame keeps them on the group path (its waiting heavy blocks cost ~2%).
+        // A/B in the environment: RRT_AB_CONT=0 off / 1 on for any launch; RRT_AB_CONT_MIN=samples
+        // left; RRT_AB_CONT_ROOM=batch blocks of room; RRT_AB_CONT_WAITERS=heavy blocks that wait
         const char* ce = std::getenv("RRT_AB_CONT");
-        const bool cont_on = !(ce && ce[0] == '0') && p->ns_aa >= 3u * p->samples_per_batch;
+        const bool part = (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
+        const bool cont_on = p->ns_aa >= 3u * p->samples_per_batch && (ce ? ce[0] == '1' : part);
         if (cont_on) {
           const uint32_t ccap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
           if (c->cont_cap < ccap) {
@@ -1716,11 +1727,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
           kp.cont_min_left = cm ? (uint32_t)std::strtoul(cm, nullptr, 10) : 2u * p->samples_per_batch;
           if (++c->cont_seq == 0) c->cont_seq = 1;
           kp.cont_seq = c->cont_seq;
+          // room for 32 heavy blocks from the launch's start (a rank's first pixels are its centre's,
+          // the costliest: their first checks come early)
           const char* cr = std::getenv("RRT_AB_CONT_ROOM");
-          // launches of at most 60% of the frame (a rank's tiles): room for 32 heavy blocks from the
-          // start; a whole frame: none (its claim queue runs most of the launch, the heavy blocks
-          // start as batch blocks leave)
-          kp.cont_room = cr ? (uint32_t)std::strtoul(cr, nullptr, 10) : ((uint64_t)kp.n_pixels * 5u <= frame_px * 3u ? 32u : 0u);
+          kp.cont_room = cr ? (uint32_t)std::strtoul(cr, nullptr, 10) : (part ? 32u : 0u);
           kp.cont_ticks = 5000000u;  // 50 ms of wall clock (100 MHz)
           const char* cw = std::getenv("RRT_AB_CONT_WAITERS");
           kp.cont_waiters = cw ? (uint32_t)std::strtoul(cw, nullptr, 10) : ~0u;
@@ -1823,8 +1833,9 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // whether the batch kernel sizes its room for it on the device (variant bits 22 / 23: A/B)
   const uint32_t hgv = (p->variant >> 28) & 0xfu, nwv = (p->variant >> 20) & 3u;
   // waves per heavy pixel: 2 (a 64-sample pixel's two steps in one round), 4 with continuations
-  // (up to 256 slots: the remaining steps of a 256-sample pixel)
-  const int heavy_nw = nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : 4;
+  // (256 slots a round: the rest of a 256-sample pixel); A/B: variant bits 20..21 = 1 / 2 / 3:
+  // 1 (2 for the point-light build) / 4 / 2
+  const int heavy_nw = nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : nwv == 2 ? 4 : 2;
   // heavy waves: hgv x the CU count (default 2), in blocks of heavy_nw waves
   const uint32_t heavy_waves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
   const uint32_t heavy_grid = std::max<uint32_t>(1u, heavy_waves / (uint32_t)heavy_nw);
@@ -1840,10 +1851,10 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // waves/SIMD: the area-light build at 4 (cfg3 15.71 -> 15.33 ms, cfg2 10.33 -> 10.01 ms against
   // 5, since the search tree took the local oversized leaves), the point-light build at 5 (cfg4
   // 14.15 ms against 14.65 at 4) -- profiles/r03_heavy_ab.md
-  const int bw = (wv >= 2 && wv <= 6) ? (int)wv : 4;
+  const int bw = (wv >= 2 && wv <= 5) ? (int)wv : 4;
   // general / Kerr builds: 3 waves/SIMD by default (cfg5: 4.56 s at 2 waves, 3.37 s at 3)
   const int gw = (wv >= 2 && wv <= 5) ? (int)wv : 3;
-  const int batch_w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 6 ? (int)wv : 5) : gw;
+  const int batch_w = lean == 1 ? bw : lean == 2 ? (wv >= 3 && wv <= 5 ? (int)wv : 5) : gw;
   uint32_t bgrid = grid;
   if (batch && kp.heavy_list) {
     // the batch grid leaves room for the heavy kernel's blocks (one per CU at most, <= 128 VGPRs
@@ -1861,6 +1872,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     }
   }
   kp.batch_waves = bgrid * 4u;
+
   // tail priority threshold (A/B: RRT_AB_PRIO_TICKS in the environment)
   kp.prio_ticks = 50000u;
   if (const char* pt = std::getenv("RRT_AB_PRIO_TICKS")) kp.prio_ticks = (uint32_t)std::strtoul(pt, nullptr, 10);
@@ -1890,7 +1902,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       HIPCHK(c, hipEventRecord(c->ev_go, stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_go, 0));
       join_guard.state = 1;
-      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, heavy_grid, 0, c->side));
+      HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, heavy_grid, RRT_HEAVY_LIST, c->side));
       HIPCHK(c, hipEventRecord(c->ev_heavy, c->side));
       join_guard.state = 2;
     }
@@ -1898,8 +1910,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
     if (kp.heavy_list) {
       HIPCHK(c, hipStreamWaitEvent(stream, c->ev_heavy, 0));
       join_guard.state = 3;
-      // continuations no heavy block took (it stopped waiting first): rendered behind both kernels
-      if (kp.cont) HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, 16u, 1, stream));
+      // continuations no block took (every waiter stopped first): rendered behind the kernels
+      if (kp.cont) HIPCHK(c, rrt_launch_heavy(c->d_kp, lean, hw, heavy_nw, 16u, RRT_HEAVY_DRAIN, stream));
     }
   } else if (path_pool) {
     std::snprintf(name, sizeof(name), "%srrt_path_kernel<%d>", deep_list ? "rrt_pixel_proof_kernel + " : "",
@@ -2353,7 +2365,8 @@ struct rrt_group {
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGetErrorString) err_str = nullptr;
-  std::vector<ncclComm_t> comm;
+  std::vector<ncclComm_t> comm;  // empty after a failed collective (the group then refuses to render)
+  decltype(&ncclCommAbort) comm_abort = nullptr;
   std::vector<int32_t*> packed;  // per member, on its device: [n_max * T^2 * 3] f32 rgb, [n_max * T^2] i32 count
   std::vector<int32_t*> inbox;   // on member 0's device, one per other member
   size_t words = 0;              // capacity of each packed / inbox buffer, int32 words
@@ -2385,7 +2398,7 @@ static int group_load_rccl(rrt_group* g) {
   };
   if (!(sym(g->comm_init_all, "ncclCommInitAll") && sym(g->comm_destroy, "ncclCommDestroy") &&
         sym(g->group_start, "ncclGroupStart") && sym(g->group_end, "ncclGroupEnd") && sym(g->send, "ncclSend") &&
-        sym(g->recv, "ncclRecv") && sym(g->err_str, "ncclGetErrorString")))
+        sym(g->recv, "ncclRecv") && sym(g->err_str, "ncclGetErrorString") && sym(g->comm_abort, "ncclCommAbort")))
     return group_fail(g, RRT_E_HIP, "RCCL lacks ncclSend / ncclRecv / ncclCommInitAll");
   std::vector<int> devs;
   for (rrt_ctx* c : g->ctx) devs.push_back(c->device);
@@ -2444,15 +2457,15 @@ extern "C" int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32
   if ((uint64_t)x0 + w > p->frame_w || (uint64_t)y0 + h > p->frame_h)
     return group_fail(g, RRT_E_INVALID, "region outside frame");
   const uint32_t n = (uint32_t)g->ctx.size(), ts = 32, T2 = ts * ts;
-  // the region's tiles, dealt block-cyclically in serpentine order
-  const uint32_t tw = (w + ts - 1) / ts, th = (h + ts - 1) / ts;
+  if (g->distinct && g->comm.empty())
+    return group_fail(g, RRT_E_HIP, "the group's RCCL communicators were aborted after a failed gather");
+  // the region's tiles, dealt block-cyclically in serpentine order (rrt_region_tiles)
   std::vector<std::vector<uint32_t>> tiles(n);
-  for (uint32_t ty = 0, k = 0; ty < th; ++ty)
-    for (uint32_t i = 0; i < tw; ++i, ++k) {
-      const uint32_t tx = (ty & 1) ? (tw - 1 - i) : i;
-      tiles[k % n].push_back(x0 + tx * ts);
-      tiles[k % n].push_back(y0 + ty * ts);
-    }
+  for (uint32_t i = 0; i < n; ++i) {
+    const int nt = rrt_region_tiles(x0, y0, w, h, ts, i, n, nullptr, 0);
+    tiles[i].resize(2 * (size_t)nt);
+    if (nt > 0) rrt_region_tiles(x0, y0, w, h, ts, i, n, tiles[i].data(), (uint32_t)nt);
+  }
   size_t n_max = 0;
   for (const auto& t : tiles) n_max = std::max(n_max, t.size() / 2);
   const size_t words = n_max * T2 * 4;
@@ -2500,13 +2513,31 @@ extern "C" int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32
   // gather to member 0: the frame's only exchange
   rrt_ctx* c0 = g->ctx[0];
   if (g->distinct) {
-    NCHK(g, g->group_start());
-    for (uint32_t i = 1; i < n; ++i) {
+    // Every member's send is paired with member 0's receive of it, both skipped together for a
+    // member without tiles (so no rank waits on a message that is never sent); each call runs
+    // with its communicator's device current.  A failed call aborts every communicator (their
+    // state after a failed group is undefined) and the group refuses later renders.
+    auto abort_all = [&](const std::string& what, ncclResult_t r) {
+      for (uint32_t i = 0; i < n && i < g->comm.size(); ++i) {
+        hipSetDevice(g->ctx[i]->device);
+        if (g->comm[i]) g->comm_abort(g->comm[i]);
+      }
+      g->comm.clear();
+      return group_fail(g, RRT_E_HIP, what + ": " + g->err_str(r));
+    };
+    ncclResult_t r = g->group_start();
+    if (r != ncclSuccess) return abort_all("ncclGroupStart", r);
+    for (uint32_t i = 1; i < n && r == ncclSuccess; ++i) {
       if (tiles[i].empty()) continue;
-      NCHK(g, g->send(g->packed[i], g->words, ncclInt32, 0, g->comm[i], g->ctx[i]->stream));
-      NCHK(g, g->recv(g->inbox[i], g->words, ncclInt32, (int)i, g->comm[0], c0->stream));
+      (void)hipSetDevice(g->ctx[i]->device);  // (no early return inside the group)
+      r = g->send(g->packed[i], g->words, ncclInt32, 0, g->comm[i], g->ctx[i]->stream);
+      if (r != ncclSuccess) break;
+      (void)hipSetDevice(c0->device);
+      r = g->recv(g->inbox[i], g->words, ncclInt32, (int)i, g->comm[0], c0->stream);
     }
-    NCHK(g, g->group_end());
+    const ncclResult_t re = g->group_end();  // closes the group even after a failed call inside it
+    if (r != ncclSuccess) return abort_all("ncclSend / ncclRecv", r);
+    if (re != ncclSuccess) return abort_all("ncclGroupEnd", re);
   } else {
     GCHK(g, hipSetDevice(c0->device));
     for (uint32_t i = 1; i < n; ++i) {

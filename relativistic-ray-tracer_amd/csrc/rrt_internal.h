@@ -183,9 +183,12 @@ struct ContRec {
   uint32_t x, y, slot, i, O;
   uint32_t seq, pad[3];
 };
-// KParams::cont_ctl words (RRT_QUEUE_STRIDE apart): records reserved, records taken, heavy blocks
-// waiting for one, batch waves exited
-enum { RRT_CONT_TAIL = 0, RRT_CONT_HEAD = 1, RRT_CONT_IDLE = 2, RRT_CONT_EXITED = 3, RRT_CONT_WORDS = 4 };
+// KParams::cont_ctl words (RRT_QUEUE_STRIDE apart): records reserved, records taken, blocks waiting
+// for one, batch waves past their last pixel (no record can come once all are)
+enum { RRT_CONT_TAIL = 0, RRT_CONT_HEAD = 1, RRT_CONT_IDLE = 2, RRT_CONT_DONE = 3, RRT_CONT_WORDS = 4 };
+// rrt_heavy_kernel launches: the heavy list then continuations (side stream), untaken records
+// behind the batch and heavy kernels (main stream)
+enum { RRT_HEAVY_LIST = 0, RRT_HEAVY_DRAIN = 1 };
 
 struct KParams {
   // scene
@@ -289,7 +292,7 @@ struct KParams {
   // continuations: a batch-kernel group whose pixel still has >= cont_min_left
   // samples to go after an adaptive check hands it to a heavy block that is waiting for work
   // (cont_ctl[RRT_CONT_IDLE] > 0), which renders the remaining steps' draw-offset slots in parallel.
-  // cont null: off.  The heavy blocks stop waiting once batch_waves batch waves have exited.
+  // cont null: off.  Waiting blocks stop once all batch_waves batch waves are past their last pixel.
   ContRec* cont;
   uint32_t* cont_ctl;
   uint32_t cont_cap, cont_min_left;
@@ -298,7 +301,6 @@ struct KParams {
   uint32_t cont_ticks;    // a heavy block stops waiting after this long without work (wall clock)
   uint32_t cont_waiters;  // heavy blocks blockIdx < cont_waiters wait for continuations; the others
                           // leave once the heavy list is done (their slots go back to the batch kernel)
-  uint32_t cont_pad;
 #if RRT_PROFILE
   // diagnostic build: per-wave progress records in host-coherent memory (RRT_WATCHDOG_MS), read by
   // the host while the kernels run: [wave][4] = {iteration, state, pixel, marker}; batch waves

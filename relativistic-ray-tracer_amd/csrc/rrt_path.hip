@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_path_kernel(const KParams* __r
 #if RRT_PROFILE
   unsigned long long pc_path = 0, pc_claim = 0, pc_trace = 0, pc_rays = 0, pc_rounds = 0;
 #endif
-  for (uint32_t round = 0;; ++round) {
+  for (;;) {  // one round
     // The launch constants are re-read from the constant cache each round: hoisted out of the loop
     // they would all stay live (in VGPRs, once the SGPRs run out) across the query
     asm volatile("" : "+s"(kpp));

@@ -50,7 +50,7 @@ __device__ __forceinline__ void park_hit(SL& cl, uint32_t t, const Isect& is0) {
 // (park_hit), re-read per light sample so no hit state stays live across the shadow queries.
 // W: the calling kernel build's tag for the out-of-line occlusion proof (rrt_device.h query_nx)
 template <bool COUNT, int LEAN, int W = 0, class SL = ShadeLds>
-__device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint32_t t, Counters& cn) {
+__device__ __forceinline__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   spec L = S(0, 0, 0);
   int total = 0;
@@ -77,7 +77,7 @@ __device__ spec direct_importance_parked(const KParams& kp, Rng& g, SL& cl, uint
   return L / (float)total;
 }
 template <bool COUNT, int LEAN, int W = 0>
-__device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
+__device__ __forceinline__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
   return direct_importance_parked<COUNT, LEAN, W>(kp, g, cl, t, cn);
@@ -85,7 +85,7 @@ __device__ spec direct_importance_lds(const KParams& kp, Rng& g, const Isect& is
 
 // estimate_direct_lighting_hemisphere (part1_code.cpp:15-31) for the parked hit
 template <bool COUNT, int LEAN>
-__device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
+__device__ __forceinline__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl, uint32_t t, Counters& cn) {
   const uint32_t bsdf = lget(cl.bsdf, t);
   const int num = (int)(kp.n_lights * kp.ns_area_light);
   spec L = S(0, 0, 0);
@@ -104,7 +104,7 @@ __device__ spec direct_hemisphere_parked(const KParams& kp, Rng& g, ShadeLds& cl
   return ((L * 2.0f) * (float)PI_D) / (float)num;
 }
 template <bool COUNT, int LEAN>
-__device__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
+__device__ __forceinline__ spec direct_hemisphere_lds(const KParams& kp, Rng& g, const Isect& is0, ColdLds& cl, uint32_t t,
                                       Counters& cn) {
   park_hit(cl, t, is0);
   return direct_hemisphere_parked<COUNT, LEAN>(kp, g, cl, t, cn);
@@ -408,9 +408,10 @@ struct GroupLds {  // group size >= 8: at most 32 groups per 256-thread block
 // it doubled the group loop's spills (cfg3 batch kernel 17.3 -> 33.5 ms), hence its own kernel.
 // The same block also takes continuations (ContRec, from the batch kernel): a pixel some of whose
 // steps are already folded, resumed from its sums and draw offset.
+// LDS: the parked hit records (ShadeLdsN, the batch kernel's own `cl` when its blocks take
+// continuations) and HeavyState (over the batch kernel's group records there).
 template <int NW>
-struct HeavyLds {
-  rrt::ShadeLdsN<64 * NW> sh;  // parked hit records (direct_importance_parked)
+struct HeavyState {
   float r[64 * NW], g[64 * NW], b[64 * NW];  // each slot's sample radiance
   uint64_t hits[NW];  // each wave's ballot of hits
   // the claimed pixel (thread 0 writes it between block barriers): position, output slot, samples
@@ -420,35 +421,80 @@ struct HeavyLds {
   uint32_t x, y, slot, i, m0;
   uint32_t go;
 };
+template <int NW>
+struct HeavyLds {
+  rrt::ShadeLdsN<64 * NW> sh;  // parked hit records (direct_importance_parked)
+  HeavyState<NW> hs;
+};
 // Thread 0: the pixel proof pass's heavy-list entry k as a fresh pixel
 template <int NW>
-__device__ __forceinline__ void heavy_take_listed(const KParams& kp, HeavyLds<NW>& hl, uint32_t k) {
+__device__ __forceinline__ void heavy_take_listed(const KParams& kp, HeavyState<NW>& hs, uint32_t k) {
   const uint32_t ts = kp.tile_size, tpix = ts * ts;
   const uint32_t ix = kp.heavy_list[k];
   const uint32_t tl = kp.tile_order[ix / tpix], r = claim_r(ix % tpix, ts);
-  hl.x = kp.tiles[2 * tl] + r % ts; hl.y = kp.tiles[2 * tl + 1] + r / ts; hl.slot = tl * tpix + r;
-  hl.i = 0; hl.m0 = 0; hl.r0 = 0.0f; hl.g0 = 0.0f; hl.b0 = 0.0f; hl.s1 = 0.0; hl.s2 = 0.0;
+  hs.x = kp.tiles[2 * tl] + r % ts; hs.y = kp.tiles[2 * tl + 1] + r / ts; hs.slot = tl * tpix + r;
+  hs.i = 0; hs.m0 = 0; hs.r0 = 0.0f; hs.g0 = 0.0f; hs.b0 = 0.0f; hs.s1 = 0.0; hs.s2 = 0.0;
 }
 // Thread 0: continuation record h once its writer has published it (seq), as the pixel to resume
 template <int NW>
-__device__ __forceinline__ void heavy_take_cont(const KParams& kp, HeavyLds<NW>& hl, uint32_t h) {
+__device__ __forceinline__ void heavy_take_cont(const KParams& kp, HeavyState<NW>& hs, uint32_t h) {
   ContRec* rc = kp.cont + h;
   while (__hip_atomic_load(&rc->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != kp.cont_seq)
     __builtin_amdgcn_s_sleep(2);  // reserved by a running batch wave, whose stores are on their way
-  hl.x = rc->x; hl.y = rc->y; hl.slot = rc->slot; hl.i = rc->i; hl.m0 = rc->O / kp.draws_miss;
-  hl.r0 = rc->r; hl.g0 = rc->g; hl.b0 = rc->b; hl.s1 = rc->s1; hl.s2 = rc->s2;
+  hs.x = rc->x; hs.y = rc->y; hs.slot = rc->slot; hs.i = rc->i; hs.m0 = rc->O / kp.draws_miss;
+  hs.r0 = rc->r; hs.g0 = rc->g; hs.b0 = rc->b; hs.s1 = rc->s1; hs.s2 = rc->s2;
+}
+__device__ __forceinline__ uint32_t cont_word(const KParams& kp, int w) {
+  return __hip_atomic_load(kp.cont_ctl + RRT_QUEUE_STRIDE * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Thread 0: take the oldest published record without waiting (true: hs holds it)
+template <int NW>
+__device__ __forceinline__ bool cont_try_take(const KParams& kp, HeavyState<NW>& hs) {
+  const uint32_t hd = cont_word(kp, RRT_CONT_HEAD);
+  uint32_t e = hd;
+  if (hd < min(cont_word(kp, RRT_CONT_TAIL), kp.cont_cap) &&
+      __hip_atomic_compare_exchange_strong(kp.cont_ctl + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, &e, hd + 1u, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    heavy_take_cont(kp, hs, hd);
+    return true;
+  }
+  return false;
+}
+// Thread 0 of a block waiting for a continuation: counts itself idle (cont_ctl[RRT_CONT_IDLE],
+// which lets the batch kernel's groups hand pixels over) while it waits, takes the next published
+// record (true), or gives up (false) once every batch wave is past its last pixel -- no record
+// can come then -- or after cont_ticks without one.  It never waits for anything else: a launch's
+// kernels may run in any order the hardware picks, and the drain launch behind them renders any
+// record left untaken.
+template <int NW>
+__device__ bool cont_wait_take(const KParams& kp, HeavyState<NW>& hs) {
+  uint32_t* const cc = kp.cont_ctl;
+  atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
+  const uint64_t since = wall_clock64();
+  bool got = false;
+  for (;;) {
+    if (cont_try_take(kp, hs)) { got = true; break; }
+    const bool fin = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_DONE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
+                     kp.batch_waves;
+    if (fin && cont_word(kp, RRT_CONT_HEAD) < min(cont_word(kp, RRT_CONT_TAIL), kp.cont_cap)) continue;  // published before
+    if (fin || wall_clock64() - since > kp.cont_ticks) break;
+    __builtin_amdgcn_s_sleep(16);
+  }
+  atomicSub(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
+  return got;
 }
 template <int LEAN, int W, int NW>
-__device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& hl, uint32_t t, rrt::Counters& cn) {
+__device__ __noinline__ void heavy_pixel_block(const KParams& kp, rrt::ShadeLdsN<64 * NW>& sh, HeavyState<NW>& hs,
+                                               uint32_t t, rrt::Counters& cn) {
   using namespace rrt;
   constexpr uint32_t NS = 64u * NW;  // slots per round
   const uint32_t Dm = kp.draws_miss, Dh = kp.draws_hit, S1 = Dh / Dm;
   const DCamera& cam = kp.cam;
-  const uint32_t x = hl.x, y = hl.y, slot = hl.slot;
+  const uint32_t x = hs.x, y = hs.y, slot = hs.slot;
   const uint64_t key = rrt_pixel_key(kp.seed, x, y);
-  spec ret = S(hl.r0, hl.g0, hl.b0);
-  double s1 = hl.s1, s2 = hl.s2;
-  uint32_t i = hl.i, m0 = hl.m0;  // samples folded; the round's first slot
+  spec ret = S(hs.r0, hs.g0, hs.b0);
+  double s1 = hs.s1, s2 = hs.s2;
+  uint32_t i = hs.i, m0 = hs.m0;  // samples folded; the round's first slot
   for (;;) {
     // the chain of the ns_aa - i samples left spans at most S1 (ns_aa - i) slots: lanes beyond
     // that are never reached by the fold and stay idle
@@ -466,21 +512,21 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
                      query_nx<false, false, false>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
     if (hit) {
-      park_hit(hl.sh, t, is);
+      park_hit(sh, t, is);
       g.ctr = sl * Dm + Dm;
-      const spec e = emission(kp.bsdfs[lget(hl.sh.bsdf, t)]);
+      const spec e = emission(kp.bsdfs[lget(sh.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else s = e + direct_importance_parked<false, LEAN, W>(kp, g, hl.sh, t, cn);
+      else s = e + direct_importance_parked<false, LEAN, W>(kp, g, sh, t, cn);
     }
     const uint64_t hb = __ballot(hit);
-    if ((t & 63u) == 0) hl.hits[t >> 6] = hb;
-    hl.r[t] = s.r; hl.g[t] = s.g; hl.b[t] = s.b;
+    if ((t & 63u) == 0) hs.hits[t >> 6] = hb;
+    hs.r[t] = s.r; hs.g[t] = s.g; hs.b[t] = s.b;
     __syncthreads();
     // the chain over the computed slots and the ordered fold (every thread alike)
     uint32_t m = 0;  // slot relative to m0
     bool st = false;
     while (m < NS) {
-      const spec sk = S(hl.r[m], hl.g[m], hl.b[m]);
+      const spec sk = S(hs.r[m], hs.g[m], hs.b[m]);
       if (sk.r != 0.0f || sk.g != 0.0f || sk.b != 0.0f) {  // zero samples: identities on the sums
         ret = ret + sk;
         const double il = illum(sk);
@@ -488,7 +534,7 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
         s2 += il * il;
       }
       ++i;
-      m += ((hl.hits[m >> 6] >> (m & 63u)) & 1ull) ? S1 : 1u;
+      m += ((hs.hits[m >> 6] >> (m & 63u)) & 1ull) ? S1 : 1u;
       st = i >= kp.ns_aa;
       if (i % kp.samples_per_batch == 0) {  // ADAPTIVE == 1 (:147-158)
         const double avg = s1 / i, sd = sqrt((s2 - avg * s1) / (i - 1));
@@ -511,23 +557,21 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, HeavyLds<NW>& 
 // The heavy pixels' kernel (heavy pixels), launched after the pixel proof pass on
 // the context's high-priority side stream, beside the batch kernel, which leaves room for its
 // blocks (rrt_host.cpp): each block of NW waves takes heavy pixels one at a time, at issue
-// priority 3 -- first the pass's heavy list, then (kp.cont) continuations from the batch kernel:
-// a block with nothing to do counts itself idle (cont_ctl[RRT_CONT_IDLE], which lets the batch
-// kernel's groups hand pixels over) and takes the next published record.  It never depends on the
-// batch kernel to finish: it stops waiting once every batch wave has exited or after cont_ticks
-// without a record, and drain (a launch behind both kernels on the main stream) renders whatever
-// records are left untaken, so an ordering of the two kernels that the hardware chooses cannot
-// hang the launch or drop a pixel.
+// priority 3 -- first the pass's heavy list, then (kp.cont, blocks below kp.cont_waiters)
+// continuations from the batch kernel (cont_wait_take).  mode RRT_HEAVY_DRAIN: the launch behind
+// the batch and heavy kernels on the main stream, which renders the records nobody took.
 template <int LEAN, int HW, int NW>
-__global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp, int drain) {
+__global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* __restrict__ kpp, int mode) {
+  const bool drain = mode == RRT_HEAVY_DRAIN;
   const KParams& kp = *kpp;
   using namespace rrt;
   __shared__ HeavyLds<NW> hl;
+  HeavyState<NW>& hs = hl.hs;
   const uint32_t t = threadIdx.x;
   Counters cn = {};
-  const uint32_t nh = drain ? 0u : min(*kp.heavy_count, kp.heavy_cap);
-  uint32_t* const cc = kp.cont_ctl;
-  bool listed = !drain, idle = false;  // (thread 0's)
+  const uint32_t nh = mode != RRT_HEAVY_LIST ? 0u : min(*kp.heavy_count, kp.heavy_cap);
+  const bool waiter = kp.cont && mode == RRT_HEAVY_LIST && blockIdx.x < kp.cont_waiters;
+  bool listed = mode == RRT_HEAVY_LIST;  // (thread 0's)
   __builtin_amdgcn_s_setprio(3);
 #if RRT_PROFILE
   volatile uint32_t* wd = kp.wd ? kp.wd + RRT_WD_HEAVY + 4u * (blockIdx.x & 0x7fffu) : nullptr;
@@ -535,65 +579,32 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
 #endif
   for (;;) {
     if (t == 0) {
-      uint32_t go = 0;
+      bool go = false;
       if (listed) {
         const uint32_t k = atomicAdd(kp.heavy_count + 1, 1u);
-        if (k < nh) { heavy_take_listed(kp, hl, k); go = 1; }
+        if (k < nh) { heavy_take_listed(kp, hs, k); go = true; }
         else listed = false;
       }
       if (!go && kp.cont && drain) {  // behind both kernels: every reserved record is written
-        const uint32_t h = atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, 1u);
-        if (h < min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap)) {
-          heavy_take_cont(kp, hl, h);
-          go = 1;
-        }
-      } else if (!go && kp.cont && blockIdx.x < kp.cont_waiters) {
-        if (!idle) { atomicAdd(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u); idle = true; }
-        uint64_t since = wall_clock64();
-        for (;;) {
-          const uint32_t hd = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t tl = min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap);
-          if (hd < tl) {
-            uint32_t e = hd;
-            if (__hip_atomic_compare_exchange_strong(cc + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, &e, hd + 1u, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-              atomicSub(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
-              idle = false;
-              heavy_take_cont(kp, hl, hd);
-              go = 1;
-              break;
-            }
-            continue;
-          }
-          // the batch kernel is done (its waves have published every record they reserved), or
-          // nothing has come for cont_ticks: stop waiting
-          const bool fin = __hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_EXITED, __ATOMIC_ACQUIRE,
-                                             __HIP_MEMORY_SCOPE_AGENT) >= kp.batch_waves;
-          if (fin && hd < min(__hip_atomic_load(cc + RRT_QUEUE_STRIDE * RRT_CONT_TAIL, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT), kp.cont_cap))
-            continue;  // published before the last wave left
-          if (fin || wall_clock64() - since > kp.cont_ticks) {
-            atomicSub(cc + RRT_QUEUE_STRIDE * RRT_CONT_IDLE, 1u);
-            idle = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(16);
-        }
+        const uint32_t h = atomicAdd(kp.cont_ctl + RRT_QUEUE_STRIDE * RRT_CONT_HEAD, 1u);
+        if (h < min(cont_word(kp, RRT_CONT_TAIL), kp.cont_cap)) { heavy_take_cont(kp, hs, h); go = true; }
+      } else if (!go && waiter) {
+        go = cont_wait_take(kp, hs);
       }
-      hl.go = go;
+      hs.go = go ? 1u : 0u;
     }
     __syncthreads();
-    const uint32_t go = hl.go;
+    const uint32_t go = hs.go;
     __syncthreads();  // every thread has read the claim before thread 0 claims again
 #if RRT_PROFILE
-    if (wd && t == 0) { wd[0] = ++wd_it; wd[1] = nh; wd[2] = hl.slot; wd[3] = 0x11u; }
+    if (wd && t == 0) { wd[0] = ++wd_it; wd[1] = nh; wd[2] = hs.slot; wd[3] = 0x11u; }
 #endif
     if (!go) break;
 #if RRT_PROFILE
     const uint64_t w_h = wall_clock64();
-    const uint32_t pslot = hl.slot;
+    const uint32_t pslot = hs.slot;
 #endif
-    heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl, t, cn);
+    heavy_pixel_block<LEAN, RRT_OCC_TAG_SLOT(LEAN, HW) ? RRT_OCC_TAG_SLOT(LEAN, HW) + 32 * NW : 0, NW>(kp, hl.sh, hs, t, cn);
 #if RRT_PROFILE
     if (wd && t == 0) wd[3] = 0x12u;  // pixel done
     if (t == 0 && pslot < (1u << 21)) {  // elapsed ticks; "rounds" 1
@@ -607,10 +618,9 @@ __global__ __launch_bounds__(64 * NW, HW) void rrt_heavy_kernel(const KParams* _
 #endif
 }
 
-// waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks; drain: the launch behind
-// the batch and heavy kernels that renders untaken continuation records
-hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, int drain, hipStream_t stream) {
-#define RRT_LAUNCH_H(L, W, N) hipLaunchKernelGGL((rrt_heavy_kernel<L, W, N>), dim3(grid), dim3(64 * N), 0, stream, d_kp, drain)
+// waves/SIMD budget 4 or 5; NW waves per pixel (1, 2 or 4); grid in blocks; mode RRT_HEAVY_*
+hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, uint32_t grid, int mode, hipStream_t stream) {
+#define RRT_LAUNCH_H(L, W, N) hipLaunchKernelGGL((rrt_heavy_kernel<L, W, N>), dim3(grid), dim3(64 * N), 0, stream, d_kp, mode)
   if (lean == 1) {
     if (waves == 5) {
       if (nw == 1) RRT_LAUNCH_H(1, 5, 1); else if (nw == 4) RRT_LAUNCH_H(1, 5, 4); else RRT_LAUNCH_H(1, 5, 2);
@@ -647,10 +657,10 @@ __device__ __forceinline__ bool cont_push(const KParams& kp, uint32_t x, uint32_
   __hip_atomic_store(&rc->seq, kp.cont_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
-// a batch wave leaves: once all have, the heavy blocks stop waiting for continuations
-__device__ __forceinline__ void cont_wave_exit(const KParams& kp, uint32_t lane) {
+// a batch wave is past its last pixel (it hands over no more): once all are, waiting blocks stop
+__device__ __forceinline__ void cont_wave_done(const KParams& kp, uint32_t lane) {
   if (kp.cont && lane == 0)
-    __hip_atomic_fetch_add(kp.cont_ctl + RRT_QUEUE_STRIDE * RRT_CONT_EXITED, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(kp.cont_ctl + RRT_QUEUE_STRIDE * RRT_CONT_DONE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int LEAN, int WAVES>
@@ -692,7 +702,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     const uint32_t nh = min(*kp.heavy_count, kp.heavy_cap);
     const uint32_t need = max((min(nh, kp.heavy_grid) * kp.heavy_nw + 3u) / 4u, kp.cont_room);
     if (blockIdx.x + min(need, gridDim.x - 1u) >= gridDim.x) {
-      cont_wave_exit(kp, lane);
+      cont_wave_done(kp, lane);
       return;
     }
   }
@@ -1067,7 +1077,7 @@ __global__ __launch_bounds__(256, WAVES) void rrt_batch_kernel(const KParams* __
     if (stop) have = false;
     RRT_ACC(t_fold, tf0);
   }
-  cont_wave_exit(kp, lane);
+  cont_wave_done(kp, lane);
 #if RRT_PROFILE
   if (wd && lane == 0) wd[3] = 0xdeadu;  // exited
 #endif
@@ -1283,14 +1293,12 @@ hipError_t rrt_launch_batch(const KParams& kp, const KParams* d_kp, int lean, in
       case 3: RRT_LAUNCH_B(1, 3); break;
       case 4: RRT_LAUNCH_B(1, 4); break;
       case 5: RRT_LAUNCH_B(1, 5); break;
-      case 6: RRT_LAUNCH_B(1, 6); break;
       default: RRT_LAUNCH_B(1, 5); break;
     }
   } else if (lean == 2) {
     switch (waves) {
       case 3: RRT_LAUNCH_B(2, 3); break;
       case 4: RRT_LAUNCH_B(2, 4); break;
-      case 6: RRT_LAUNCH_B(2, 6); break;
       default: RRT_LAUNCH_B(2, 5); break;
     }
   } else if (lean == rrt::V_KERR) {  // general builds: waves/SIMD as an A/B knob

@@ -101,7 +101,7 @@ class Stats(C.Structure):
 # every symbol include/rrt.h declares (checked by tests/test_capi_host.py)
 EXPORTS = ["rrt_abi_version", "rrt_create", "rrt_destroy", "rrt_last_error", "rrt_set_scene", "rrt_set_camera",
            "rrt_set_spacetime", "rrt_render_params_default", "rrt_render", "rrt_render_tiles_device",
-           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_get_stats", "rrt_get_launch_times", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree", "rrt_get_search_tree", "rrt_proof_envelope",
+           "rrt_unpack_tiles_device", "rrt_tonemap_device", "rrt_partition_tiles", "rrt_region_tiles", "rrt_get_stats", "rrt_get_launch_times", "rrt_get_bvh", "rrt_get_free_grid", "rrt_get_clean_tree", "rrt_get_search_tree", "rrt_proof_envelope",
            "rrt_scene_file_load", "rrt_scene_file_desc", "rrt_scene_file_free", "rrt_camera_file_load",
            "rrt_scene_file_save", "rrt_collada_options_default", "rrt_collada_load", "rrt_camera_settings_load",
            "rrt_camera_settings_save", "rrt_camera_state_file_load", "rrt_camera_state_file_save",
@@ -153,6 +153,8 @@ def lib():
                                               vp]
         L.rrt_tonemap_device.argtypes = [vp, C.c_uint32, vp, vp, vp]
         L.rrt_partition_tiles.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32]
+        if hasattr(L, "rrt_region_tiles"):  # absent from older builds loaded through RRT_LIB
+            L.rrt_region_tiles.argtypes = [C.c_uint32] * 7 + [vp, C.c_uint32]
         L.rrt_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.rrt_get_launch_times.argtypes = [vp, C.c_uint32, vp, vp]
         L.rrt_libm_eval.argtypes = [vp, C.c_int, vp, vp, vp, C.c_uint64]
@@ -337,6 +339,16 @@ def partition_tiles(frame_w, frame_h, tile_size, rank, world):
         raise RRTError(n, "bad partition arguments")
     out = np.zeros((max(n, 1), 2), np.uint32)
     lib().rrt_partition_tiles(frame_w, frame_h, tile_size, rank, world, out.ctypes.data, n)
+    return out[:n]
+
+
+def region_tiles(x0, y0, w, h, tile_size, rank, world):
+    """rrt_region_tiles: rank's tiles of the region's block-cyclic deal (rrt_group_render's split)."""
+    n = lib().rrt_region_tiles(x0, y0, w, h, tile_size, rank, world, None, 0)
+    if n < 0:
+        raise RRTError(n, "bad partition arguments")
+    out = np.zeros((max(n, 1), 2), np.uint32)
+    lib().rrt_region_tiles(x0, y0, w, h, tile_size, rank, world, out.ctypes.data, n)
     return out[:n]
 
 

@@ -108,15 +108,12 @@ class Case:
 
     @property
     def exact(self):
-        """Cases the GPU must match bit for bit: every case whose scene has no microfacet BSDF.
-        The per-sample sin/cos (bounces, environment light), acos/atan2 (environment light,
-        hemisphere sampler) and sinf/cosf (hemisphere sampler) are the host C library's own
-        routines restated on the device (csrc/rrt_glibm.h, tests/test_glibm.py).  The microfacet
-        BSDF's exp/log/erf/atan/tan are restated too (bit-exact through rrt_libm_eval,
-        tests/test_gpu_glibm.py) but the kernels call the device libm for them (rrt_device.h
-        RRT_MF_GLIBM: compiled in, the restatements made the general builds fault),
-        so those cases are held to the north-star per-pixel bound instead."""
-        return "microfacet" not in self.info.get("dae", "")
+        """Cases the GPU must match bit for bit: every case.  The per-sample sin/cos (bounces,
+        environment light), acos/atan2 (environment light, hemisphere sampler), sinf/cosf
+        (hemisphere sampler) and the microfacet BSDF's exp/log/erf/atan/tan are the host C
+        library's own routines restated on the device (csrc/rrt_glibm.h, tests/test_glibm.py,
+        tests/test_gpu_glibm.py)."""
+        return True
 
 
 def all_cases():

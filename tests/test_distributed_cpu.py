@@ -89,3 +89,51 @@ def test_plan_layout():
     plan = rrt_frame.FramePlan(1920, 1080, 8)
     assert plan.n_max == len(plan.tiles(0)) and sum(len(plan.tiles(q)) for q in range(8)) == 60 * 34
     assert plan.words == plan.n_max * 1024 * 4
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 6, 7, 8])
+def test_tile_deal_matches_frame_plan(world):
+    """The library's block-cyclic deal (rrt_partition_tiles for bench.py's ranks, rrt_region_tiles
+    for rrt_group_render's members) against rrt_frame.FramePlan, on the BASELINE frame sizes and a
+    ragged region: every tile of the frame or region exactly once, in serpentine order, tile k to
+    rank k % world; a rank may get no tile; the packed layout's capacity holds the largest share;
+    unpacking a synthetic packed frame through the plan restores every pixel."""
+    import rrt
+
+    for W, H in [(480, 360), (1920, 1080), (3840, 2160), (100, 40)]:
+        plan = rrt_frame.FramePlan(W, H, world)
+        tw, th = (W + 31) // 32, (H + 31) // 32
+        order = [((i if ty % 2 == 0 else tw - 1 - i) * 32, ty * 32) for ty in range(th) for i in range(tw)]
+        for q in range(world):
+            want = np.array(order[q::world], np.uint32).reshape(-1, 2)
+            assert np.array_equal(plan.tiles(q), want)
+            assert np.array_equal(rrt.region_tiles(0, 0, W, H, 32, q, world), want)
+        assert plan.n_max == max(len(plan.tiles(q)) for q in range(world))
+        assert sorted(map(tuple, np.concatenate([plan.tiles(q) for q in range(world)]).tolist())) == sorted(order)
+    # a region (rrt_group_render): tiles from the region's origin, the same deal
+    x0, y0, w, h = 70, 13, 200, 65
+    rt = [rrt.region_tiles(x0, y0, w, h, 32, q, world) for q in range(world)]
+    full = [tuple(t) for q in range(world) for t in rt[q].tolist()]
+    assert len(full) == len(set(full)) == ((w + 31) // 32) * ((h + 31) // 32)
+    assert all(x0 <= x < x0 + w and y0 <= y < y0 + h and (x - x0) % 32 == 0 and (y - y0) % 32 == 0 for x, y in full)
+    if world > len(full):
+        assert any(len(t) == 0 for t in rt)
+    # packed layout round trip (rrt_frame.unpack_host, the rrt_unpack_kernel mapping)
+    W, H = 100, 40
+    plan = rrt_frame.FramePlan(W, H, world)
+    rng = np.random.default_rng(world)
+    frame = rng.random((H, W, 3), dtype=np.float32)
+    cnt = rng.integers(1, 1 << 20, (H, W), dtype=np.int32)
+    bufs = []
+    for q in range(world):
+        b = np.full(plan.words, -1, np.int32)
+        prgb = b[:plan.count_offset].view(np.float32).reshape(-1, 32, 32, 3)
+        pcnt = b[plan.count_offset:].reshape(-1, 32, 32)
+        for t, (x, y) in enumerate(plan.tiles(q)):
+            x, y = int(x), int(y)
+            tw, th = min(32, W - x), min(32, H - y)
+            prgb[t, :th, :tw] = frame[y:y + th, x:x + tw]
+            pcnt[t, :th, :tw] = cnt[y:y + th, x:x + tw]
+        bufs.append(b)
+    rgb2, cnt2 = rrt_frame.unpack_host(plan, bufs)
+    assert np.array_equal(rgb2.view(np.uint32), frame.view(np.uint32)) and np.array_equal(cnt2, cnt)

@@ -4,8 +4,8 @@ against the CPU restatement (oracle/restate ro_render with bh_kind = Kerr) on th
 Parity against the reference is UNPINNED (the reference has no Kerr metric); the restatement is
 pinned by physics in tests/test_kerr_oracle.py.  The Kerr march uses only + - * / sqrt, and the
 per-sample sin/cos/acos/atan2/sinf/cosf are the host C library's own routines restated on the
-device (rrt_glibm.h), so the same exactness rule as the reference cases applies: every case
-without a microfacet BSDF is bit-exact (RGB, sample counts, RNG draws)."""
+device (rrt_glibm.h), the microfacet BSDF's exp/log/erf/atan/tan too, so the same exactness rule
+as the reference cases applies: every case is bit-exact (RGB, sample counts, RNG draws)."""
 import numpy as np
 import pytest
 

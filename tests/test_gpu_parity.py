@@ -1,11 +1,10 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's golden outputs.
 
-Every case without a microfacet BSDF (Case.exact) must be bit-exact, including the per-pixel
-sample counts and RNG draw counts: the bounce, hemisphere and environment paths' sin/cos/acos/
-atan2/sinf/cosf are the host C library's own routines restated on the device (rrt_glibm.h).
-The microfacet cases (tan/exp/log/atan/erf from the device libm in the kernels, rrt_device.h
-RRT_MF_GLIBM) are held to the north-star tolerance on every pixel: max over pixels of the
-per-pixel L2 of linear HDR RGB <= 1e-4."""
+Every case (Case.exact) must be bit-exact, including the per-pixel sample counts and RNG draw
+counts: the bounce, hemisphere, environment and microfacet paths' sin/cos/acos/atan2/sinf/cosf/
+exp/log/erf/atan/tan are the host C library's own routines restated on the device
+(rrt_glibm.h).  (check() keeps the north-star bound -- max per-pixel L2 of linear HDR RGB <= 1e-4
+-- for any case marked inexact.)"""
 import os
 
 import numpy as np
