@@ -262,10 +262,12 @@ def test_two_streams_one_context(gpu):
 
 
 # Continuations: pixels of >= 3 adaptive steps that have not stopped at a check are
-# handed from the batch kernel to waiting heavy blocks.  Modes: the library default; "eager" hands
-# over every pixel that did not stop (RRT_AB_CONT_MIN=1) with room for 64 heavy blocks from the
+# handed from the batch kernel to waiting heavy blocks (by default in launches of <= 60% of the
+# frame: the crops).  Modes: the library default; "eager" hands over every pixel that did not stop
+# (RRT_AB_CONT_MIN=1), in any launch (RRT_AB_CONT=1), with room for 64 heavy blocks from the
 # launch's start; "off" (RRT_AB_CONT=0).  Read by the library at every launch.
-CONT_MODES = {"default": {}, "eager": {"RRT_AB_CONT_MIN": "1", "RRT_AB_CONT_ROOM": "64"}, "off": {"RRT_AB_CONT": "0"}}
+CONT_MODES = {"default": {}, "eager": {"RRT_AB_CONT": "1", "RRT_AB_CONT_MIN": "1", "RRT_AB_CONT_ROOM": "64"},
+              "off": {"RRT_AB_CONT": "0"}}
 CONT_CASES = ["cfg4_knot_4k_s256_crop", "cfg4_knot_4k_s256_crop2", "cfg4_knot_4k_s256_crop3", "spheres_96x72_s64_a16"]
 
 

@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--tile", type=int, default=32, help="tile size of the split (bench.py: 32)")
-    ap.add_argument("--split", default="lib", help="lib (rrt_partition_tiles) or latS: rank = (tx + S ty) % world")
+    ap.add_argument("--split", default="lib", help="lib (rrt_partition_tiles), latS: rank = (tx + S ty) %% world, "
+                    "serS: serpentine index k, rank = (k + S ty) %% world")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
@@ -46,6 +47,12 @@ def main():
     r.set_black_hole(*wl["bh"], **({"spin": kerr[0], "axis": kerr[1]} if kerr else {}))
     if a.split == "lib":
         sets = [rrt.partition_tiles(W, H, ts, k, a.world) for k in range(a.world)]
+    elif a.split.startswith("ser"):  # serpentine order, tile k of row ty to rank (k + S ty) % world
+        sm = int(a.split[3:])
+        tw, th = (W + ts - 1) // ts, (H + ts - 1) // ts
+        order = [((i if ty % 2 == 0 else tw - 1 - i), ty) for ty in range(th) for i in range(tw)]
+        sets = [np.array([(tx * ts, ty * ts) for k, (tx, ty) in enumerate(order) if (k + sm * ty) % a.world == q],
+                         np.uint32).reshape(-1, 2) for q in range(a.world)]
     else:  # A/B of other splits: a 2-D lattice of tiles over the ranks
         sm = int(a.split[3:])
         tw, th = (W + ts - 1) // ts, (H + ts - 1) // ts
@@ -58,6 +65,10 @@ def main():
     fcnt = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     times, sums, digests, verified = {v: [] for v in a.variants}, {}, {}, {}
+    # warm-up (the first launch of a process loads the kernels): rank 0's tiles once, untimed
+    r.render_tiles_device(rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=wl.get("depth", 1)), sets[0], ts,
+                          prgb.data_ptr(), pcnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
     per_rank = {v: [[] for _ in sets] for v in a.variants}
     for _ in range(a.rounds):
         for v in a.variants:
