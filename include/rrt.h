@@ -293,7 +293,7 @@ int rrt_tonemap_device(rrt_ctx* ctx, uint32_t n_pixels, const float* d_rgb, uint
 
 /* Multi-GPU group: one frame region over several contexts, one per GPU (the
  * reference's tile worker pool, pathtracer.cpp:251-255, 279-281, 611-644, as one launch per GPU).
- * The region's 32x32 tiles are dealt block-cyclically (serpentine), every member renders its
+ * The region's 32x32 tiles are dealt over the members as a lattice (rrt_region_tiles), every member renders its
  * tiles into a packed buffer on its own stream, member 0 gathers them -- RCCL grouped
  * send / recv over xGMI when the members are on distinct devices, device copies when several
  * share one -- and unpacks them.  Output as rrt_render (host buffers [h][w]).  The contexts must
@@ -304,9 +304,10 @@ int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32_t x0, uint
                      float* rgb_out, int32_t* count_out, const volatile int* cancel);
 void rrt_group_destroy(rrt_group* g);
 
-/* Block-cyclic tile partition of a frame over `world` ranks (serpentine 32x32 tile order,
- * multi-GPU split of SURVEY 8(e)).  Writes up to max_tiles (x, y) pairs for `rank` into
- * tiles_out and returns the number of tiles (or a negative error). */
+/* Tile partition of a frame over `world` ranks (the multi-GPU split of SURVEY 8(e)): tile (tx, ty)
+ * goes to rank (tx + S ty) % world, S the integer nearest 0.382 world that is prime to it (1 for
+ * world <= 4, 2 for 5, 3 for 7 and 8), tiles listed row by row.  Writes up to max_tiles (x, y)
+ * pairs for `rank` into tiles_out and returns the number of tiles (or a negative error). */
 int rrt_partition_tiles(uint32_t frame_w, uint32_t frame_h, uint32_t tile_size, uint32_t rank, uint32_t world,
                         uint32_t* tiles_out, uint32_t max_tiles);
 /* The same deal over the tiles of a region (x0, y0, w x h pixels; tiles from its origin): the split

@@ -1265,16 +1265,33 @@ extern "C" void rrt_kerr_frame(const double* axis, double* ex, double* ey, doubl
   ey[2] = ez[0] * ex[1] - ez[1] * ex[0];
 }
 
-// The block-cyclic serpentine deal of a region's tiles (origin x0, y0; w x h pixels) over `world`
-// ranks: tile k of the serpentine order (rows alternate direction) goes to rank k % world.
+// The lattice deal of a region's tiles (origin x0, y0; w x h pixels) over `world` ranks: tile
+// (tx, ty) goes to rank (tx + S ty) % world, S = rrt_deal_stride(world) -- every row dealt
+// cyclically, each row shifted by S, so a rank's tiles form a sheared lattice: no rank owns whole
+// columns (the serpentine order k % world did when the row length is a multiple of world: a 4K
+// frame's 120 tiles a row), and a cluster of costly tiles spreads over every rank.  Measured, every
+// rank's tiles timed on one MI355X, slowest of 8 ranks (profiles/r06_deal_w8.txt): cfg4 3.71 ->
+// 3.26 ms, cfg3 3.24 -> 3.16 ms against the serpentine deal.
+static uint32_t rrt_deal_stride(uint32_t world) {
+  // the integer nearest 0.382 world that is prime to it (2 -> 1, 4 -> 1, 5 -> 2, 7 -> 3, 8 -> 3)
+  uint32_t best = 1;
+  double bd = 1e300;
+  for (uint32_t s = 1; s < world; ++s) {
+    uint32_t a = s, b = world;
+    while (b) { const uint32_t t = a % b; a = b; b = t; }
+    const double d = std::fabs((double)s - 0.382 * world);
+    if (a == 1 && d < bd) { bd = d; best = s; }
+  }
+  return best;
+}
 extern "C" int rrt_region_tiles(uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t ts, uint32_t rank,
                                 uint32_t world, uint32_t* out, uint32_t max_tiles) {
   if (ts == 0 || world == 0 || rank >= world) return RRT_E_INVALID;
-  uint32_t tw = (w + ts - 1) / ts, th = (h + ts - 1) / ts, n = 0, k = 0;
+  const uint32_t tw = (w + ts - 1) / ts, th = (h + ts - 1) / ts, S = rrt_deal_stride(world);
+  uint32_t n = 0;
   for (uint32_t ty = 0; ty < th; ++ty) {
-    for (uint32_t i = 0; i < tw; ++i, ++k) {
-      uint32_t tx = (ty & 1) ? (tw - 1 - i) : i;  // serpentine
-      if (k % world != rank) continue;
+    for (uint32_t tx = 0; tx < tw; ++tx) {
+      if ((uint32_t)(((uint64_t)tx + (uint64_t)S * ty) % world) != rank) continue;
       if (out && n < max_tiles) { out[2 * n] = x0 + tx * ts; out[2 * n + 1] = y0 + ty * ts; }
       ++n;
     }
@@ -1567,6 +1584,36 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // hit, which holds at depth <= 1 (jitter + the direct-lighting samplers).
   const bool batch = !deep && !count && !pixel_loop && std::min(p->ns_aa, p->samples_per_batch) >= 5 &&
                      !(p->flags & RRT_RENDER_PER_PIXEL);
+  // Continuations (rrt_sample.hip cont_push): the records, their control words and
+  // the heavy blocks' waiting policy.  A/B in the environment: RRT_AB_CONT_MIN=samples left;
+  // RRT_AB_CONT_ROOM=batch blocks of room; RRT_AB_CONT_WAITERS=heavy blocks that wait.  false: HIP error
+  auto setup_cont = [&](bool part) -> bool {
+    const uint32_t ccap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
+    if (c->cont_cap < ccap) {
+      hipFree(c->d_cont); c->d_cont = nullptr; c->cont_cap = 0;
+      if (hipMalloc(&c->d_cont, sizeof(ContRec) * ccap) != hipSuccess ||
+          hipMemset(c->d_cont, 0, sizeof(ContRec) * ccap) != hipSuccess) {
+        fail(c, RRT_E_HIP, "continuation records: allocation failed");
+        return false;
+      }
+      c->cont_cap = ccap;
+    }
+    kp.cont = c->d_cont;
+    kp.cont_ctl = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);
+    kp.cont_cap = (uint32_t)c->cont_cap;
+    const char* cm = std::getenv("RRT_AB_CONT_MIN");
+    kp.cont_min_left = cm ? (uint32_t)std::strtoul(cm, nullptr, 10) : 2u * p->samples_per_batch;
+    if (++c->cont_seq == 0) c->cont_seq = 1;
+    kp.cont_seq = c->cont_seq;
+    // room for 32 heavy blocks from the launch's start (a rank's first pixels are its centre's,
+    // the costliest: their first checks come early)
+    const char* cr = std::getenv("RRT_AB_CONT_ROOM");
+    kp.cont_room = cr ? (uint32_t)std::strtoul(cr, nullptr, 10) : (part ? 32u : 0u);
+    kp.cont_ticks = 5000000u;  // 50 ms of wall clock (100 MHz)
+    const char* cw = std::getenv("RRT_AB_CONT_WAITERS");
+    kp.cont_waiters = cw ? (uint32_t)std::strtoul(cw, nullptr, 10) : ~0u;
+    return true;
+  };
   if (batch) {
     kp.draws_miss = 2;
     uint32_t dh = 2;
@@ -1712,30 +1759,29 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
         const char* ce = std::getenv("RRT_AB_CONT");
         const bool part = (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
         const bool cont_on = p->ns_aa >= 3u * p->samples_per_batch && (ce ? ce[0] == '1' : part);
-        if (cont_on) {
-          const uint32_t ccap = std::min<uint32_t>(kp.n_pixels, std::max<uint32_t>(4096u, kp.n_pixels / 256u));
-          if (c->cont_cap < ccap) {
-            hipFree(c->d_cont); c->d_cont = nullptr;
-            HIPCHK(c, hipMalloc(&c->d_cont, sizeof(ContRec) * ccap));
-            HIPCHK(c, hipMemset(c->d_cont, 0, sizeof(ContRec) * ccap));
-            c->cont_cap = ccap;
-          }
-          kp.cont = c->d_cont;
-          kp.cont_ctl = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 2);
-          kp.cont_cap = (uint32_t)c->cont_cap;
-          const char* cm = std::getenv("RRT_AB_CONT_MIN");
-          kp.cont_min_left = cm ? (uint32_t)std::strtoul(cm, nullptr, 10) : 2u * p->samples_per_batch;
-          if (++c->cont_seq == 0) c->cont_seq = 1;
-          kp.cont_seq = c->cont_seq;
-          // room for 32 heavy blocks from the launch's start (a rank's first pixels are its centre's,
-          // the costliest: their first checks come early)
-          const char* cr = std::getenv("RRT_AB_CONT_ROOM");
-          kp.cont_room = cr ? (uint32_t)std::strtoul(cr, nullptr, 10) : (part ? 32u : 0u);
-          kp.cont_ticks = 5000000u;  // 50 ms of wall clock (100 MHz)
-          const char* cw = std::getenv("RRT_AB_CONT_WAITERS");
-          kp.cont_waiters = cw ? (uint32_t)std::strtoul(cw, nullptr, 10) : ~0u;
-        }
+        if (cont_on && !setup_cont(part)) return RRT_E_HIP;
       }
+    }
+  }
+  // Kerr continuations.  The Kerr build has no pixel pass (the miss proofs are
+  // the Schwarzschild stepper's), so no heavy list; in launches of at most 60% of the frame (a
+  // rank's share) of three or more adaptive steps a pixel, its groups hand a pixel with two or more
+  // steps to go to a waiting heavy block of the Kerr build (256 draw-offset slots a round).  cfg5
+  // (1024 spp) split 8 ways ended each rank's launch on a few pixels of 32 steps near the hole.
+  if (batch && kerr && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 && !(p->flags & RRT_RENDER_NO_HEAVY)) {
+    const uint64_t frame_px = (uint64_t)p->frame_w * p->frame_h;
+    const bool part = (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
+    const char* ce = std::getenv("RRT_AB_CONT");
+    if (p->ns_aa >= 3u * p->samples_per_batch && (ce ? ce[0] == '1' : part)) {
+      if (c->heavy_list_cap < 1) {  // the kernels read the (empty) list's counters
+        hipFree(c->d_heavy_list); c->d_heavy_list = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_heavy_list, sizeof(uint32_t) * 4096u));
+        c->heavy_list_cap = 4096u;
+      }
+      kp.heavy_list = c->d_heavy_list;
+      kp.heavy_count = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);
+      kp.heavy_cap = 0;
+      if (!setup_cont(part)) return RRT_E_HIP;
     }
   }
   // The bounce (depth >= 2) per-pixel-loop kernel behind the pixel miss proof pass: a proven
@@ -1835,7 +1881,8 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // waves per heavy pixel: 2 (a 64-sample pixel's two steps in one round), 4 with continuations
   // (256 slots a round: the rest of a 256-sample pixel); A/B: variant bits 20..21 = 1 / 2 / 3:
   // 1 (2 for the point-light build) / 4 / 2
-  const int heavy_nw = nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : nwv == 2 ? 4 : 2;
+  const int heavy_nw = lean == 3 ? 4 /* the Kerr build's only heavy kernel */
+                       : nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : nwv == 2 ? 4 : 2;
   // heavy waves: hgv x the CU count (default 2), in blocks of heavy_nw waves
   const uint32_t heavy_waves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
   const uint32_t heavy_grid = std::max<uint32_t>(1u, heavy_waves / (uint32_t)heavy_nw);
@@ -2344,7 +2391,7 @@ extern "C" int rrt_camera_file_load(const char* path, rrt_camera_desc* out) {
 // ------------------------------------------------------------------------------ device groups
 // One frame region over several contexts (one per GPU): the reference's worker pool over tiles
 // (pathtracer.cpp:251-255, 279-281, 611-644) as one launch per GPU.  The region's 32x32 tiles
-// are dealt block-cyclically in serpentine order (rrt_partition_tiles' rule), every member renders
+// are dealt over the members as a lattice (rrt_partition_tiles' rule), every member renders
 // its tiles into one packed buffer on its own stream, and the buffers are gathered to member 0
 // -- over RCCL (grouped ncclSend / ncclRecv, xGMI between MI355X) when the members sit on
 // distinct devices, by device copies when several members share one device (a one-GPU run of
@@ -2459,7 +2506,7 @@ extern "C" int rrt_group_render(rrt_group* g, const rrt_render_params* p, uint32
   const uint32_t n = (uint32_t)g->ctx.size(), ts = 32, T2 = ts * ts;
   if (g->distinct && g->comm.empty())
     return group_fail(g, RRT_E_HIP, "the group's RCCL communicators were aborted after a failed gather");
-  // the region's tiles, dealt block-cyclically in serpentine order (rrt_region_tiles)
+  // the region's tiles, dealt over the members as a lattice (rrt_region_tiles)
   std::vector<std::vector<uint32_t>> tiles(n);
   for (uint32_t i = 0; i < n; ++i) {
     const int nt = rrt_region_tiles(x0, y0, w, h, ts, i, n, nullptr, 0);

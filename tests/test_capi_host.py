@@ -87,7 +87,9 @@ def test_partition_covers_frame_once(world):
             seen[(int(x), int(y))] = r
     assert len(seen) == ((W + ts - 1) // ts) * ((H + ts - 1) // ts)
     sizes = [sum(1 for v in seen.values() if v == r) for r in range(world)]
-    assert max(sizes) - min(sizes) <= 1
+    # the lattice deal: every row dealt cyclically (shares differ by one a row), every `world`
+    # consecutive rows give each rank the same share, so the leftover rows bound the difference
+    assert max(sizes) - min(sizes) <= max(1, (H + ts - 1) // ts % world)
 
 
 def test_partition_load_balance_cfg3():

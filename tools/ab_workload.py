@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--tile", type=int, default=32, help="tile size of the split (bench.py: 32)")
     ap.add_argument("--split", default="lib", help="lib (rrt_partition_tiles), latS: rank = (tx + S ty) %% world, "
                     "serS: serpentine index k, rank = (k + S ty) %% world")
+    ap.add_argument("--rotate", action="store_true", help="round r renders the ranks from rank r %% world on "
+                    "(a rank's time must not depend on its place in the sequence)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
@@ -70,7 +72,7 @@ def main():
                           prgb.data_ptr(), pcnt.data_ptr(), stream=s)
     torch.cuda.synchronize()
     per_rank = {v: [[] for _ in sets] for v in a.variants}
-    for _ in range(a.rounds):
+    for rnd in range(a.rounds):
         for v in a.variants:
             var, _, rest = v.partition(":")
             fl, _, envs = rest.partition(":")  # VARIANT:FLAGS:NAME=VALUE,... (library A/B switches read per launch)
@@ -84,7 +86,9 @@ def main():
             worst = 0.0
             frgb.view(torch.int32).fill_(-1)
             fcnt.fill_(-1)
-            for k, tiles in enumerate(sets):
+            seq = [(rnd + j) % len(sets) for j in range(len(sets))] if a.rotate else range(len(sets))
+            for k in seq:
+                tiles = sets[k]
                 prgb.view(torch.int32).fill_(-1)  # poison: stale slots of an earlier rank cannot leak
                 pcnt.fill_(-1)
                 r.render_tiles_device(p, tiles, ts, prgb.data_ptr(), pcnt.data_ptr(), stream=s)

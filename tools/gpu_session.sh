@@ -133,6 +133,28 @@ for step in "$@"; do
     benchall) run bench 600 python3 bench.py --steps 5 --warmup 2 && run bench2 600 python3 bench.py --workload cfg2 --steps 5 --warmup 2 &&
               run bench4 600 python3 bench.py --workload cfg4 --steps 2 --warmup 1 && run bench5 900 python3 bench.py --workload cfg5 --steps 1 --warmup 1 &&
               run benchm3 900 python3 bench.py --workload m3 --steps 2 --warmup 1 ;;
+    abfresh) # fresh-pixel continuations for the launch's last claims (cfg3 8-way), rounds 3
+           run abfresh 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 0 0:0:RRT_AB_CONT_FRESH=2048 0:0:RRT_AB_CONT_FRESH=8192 0:0:RRT_AB_CONT_FRESH=32768 ;;
+    abdeal) # tile deals of the 8-way split: serpentine (lib), serpentine + row offset S (serS), lattice (latS)
+           for wl in cfg5 cfg3 cfg4; do for sp in lib ser1 ser3 lat3; do
+             run abdeal_${wl}_$sp 600 python3 tools/ab_workload.py --workload $wl --world 8 --rounds 2 --split $sp 0 || exit $?; done; done ;;
+    abdeal2) # lattice deals (rank = (tx + S ty) % 8) against the serpentine, ranks in rotated order; cfg4 heavy blocks of 8 waves
+           run abnw8 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate --split lat3 0 0:0:RRT_AB_HEAVY_NW=8 0:0:RRT_AB_HEAVY_NW=2 || exit $?
+           for wl in cfg4 cfg3 cfg5; do for sp in lib lat1 lat3 lat5; do
+             [ $wl = cfg5 ] && [ $sp = lat1 ] && continue
+             run abdeal2_${wl}_$sp 600 python3 tools/ab_workload.py --workload $wl --world 8 --rounds 3 --rotate --split $sp 0 || exit $?; done; done ;;
+    phase5r) # cfg5 rank 0 (slowest) and rank 3 of the 8-way split on the profile build: slowest pixels, per-pixel times
+           RRT_LIB=tools/librrt_prof.so run ph5_r0 300 python3 tools/phase_profile.py --workload cfg5 --flags 0 --rank 0 8 &&
+           RRT_LIB=tools/librrt_prof.so run ph5_r3 300 python3 tools/phase_profile.py --workload cfg5 --flags 0 --rank 3 8 ;;
+    kcont) # Kerr continuations: parity on cfg5's framing, then the 8-way split with / without them and 16-px tiles
+           run pytest_kcont 900 python3 -u -m pytest tests/test_gpu_kerr.py -x -q -s --timeout 600 --timeout-method thread -k cfg5_framing &&
+           run abk8 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate 0 0:0:RRT_AB_CONT=0 &&
+           run abk8t16 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate --tile 16 0 0:0:RRT_AB_CONT=0 &&
+           run ab38 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 --rotate 0 &&
+           run ab48 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate 0 ;;
+    phase4r) # cfg4 ranks 6 and 3 of the 8-way (lattice) split on the profile build
+           RRT_LIB=tools/librrt_prof.so run ph4_r6 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 --rank 6 8 &&
+           RRT_LIB=tools/librrt_prof.so run ph4_r3 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 --rank 3 8 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
