@@ -12,7 +12,7 @@ generated 100k-triangle torus-knot scene (rrt_scenes.py; CBdragon.dae is missing
 with the generated HDR sky environment map, CBbunny at 3840x2160, 1024 spp.
 
 One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's 32x32
-tiles are split block-cyclically (rrt_partition_tiles); every rank renders its tiles into a
+tiles are dealt over the ranks as a lattice (rrt_partition_tiles); every rank renders its tiles into a
 packed buffer and rank 0 gathers them over RCCL and unpacks them into the frame (the only
 exchange step).  Total work is fixed, so scaling is "strong".
 
@@ -53,7 +53,7 @@ WORKLOADS = {
                depth=3, desc="m3: CBspheres_lambertian.dae 1920x1080 64spp, Schwarzschild, max_ray_depth 3 "
                              "(at_least_one_bounce_radiance, part1_code.cpp:69-101)"),
     "cfg5": dict(dae="CBbunny.dae", w=3840, h=2160, spp=1024, bh=((0.0, 1.0, 0.0), 0.1, 0.1), row_stride=24,
-                 kerr=(0.9, (0.0, 1.0, 0.0)), env="@sky",
+                 kerr=(0.9, (0.0, 1.0, 0.0)), env="@sky", tile=16,
                  desc="cfg5: CBbunny.dae 3840x2160 1024spp, Kerr a/M 0.9 (axis +y, r_s 0.1, dtheta 0.1) + "
                       "1024x512 HDR sky envmap, depth 1"),
 }
@@ -116,7 +116,9 @@ def load_workload_scene(wl, workdir):
     rc = rrt.lib().rrt_camera_state_file_save(cpath.encode(), cam)
     assert rc == 0
     return scene, cam, spath, cpath
-TILE = 32
+TILE = 32  # the split's tile side; cfg5 deals 16-px tiles (WORKLOADS "tile"): its cost sits in the lensed
+           # ring around the hole, and finer tiles spread it over the ranks (8-way slowest rank 243 -> 217 ms,
+           # profiles/r06_deal_w8.txt); cfg3 / cfg4 are faster at 32 (3.15 vs 3.23 ms, 3.03 vs 3.23 ms)
 AUDIT_EVERY_LOG2 = 10  # proof audit: every 1024th proven ray / pixel of the executed-work pass
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_AABB, BYTES_PRIM, BYTES_PIXEL = 48, 72, 16  # SURVEY 8(d) algorithmic bytes
@@ -351,7 +353,8 @@ def main():
     depth = wl.get("depth", 1)
     params = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=depth, variant=a.variant)
 
-    plan = rrt_frame.FramePlan(W, H, world, TILE)
+    tile = wl.get("tile", TILE)
+    plan = rrt_frame.FramePlan(W, H, world, tile)
     tiles = plan.tiles(rank)
     tpix = plan.tpix
     # packed per-rank result (rrt_frame.py layout): f32 rgb then i32 counts
@@ -376,13 +379,13 @@ def main():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        r.render_tiles_device(params, tiles, TILE, p_rgb, p_cnt, stream=s_handle)
+        r.render_tiles_device(params, tiles, tile, p_rgb, p_cnt, stream=s_handle)
         e1.record(stream)
         bufs = rrt_frame.gather(dist, packed, rank, world)  # RCCL over xGMI; the only exchange
         if rank == 0:
             for q in range(world):
                 base = bufs[q].data_ptr()
-                r.unpack_tiles_device(plan.tiles(q), TILE, W, H, base, base + plan.count_offset * 4,
+                r.unpack_tiles_device(plan.tiles(q), tile, W, H, base, base + plan.count_offset * 4,
                                       frame_rgb.data_ptr(), frame_cnt.data_ptr(), stream=s_handle)
         if timed:
             kern_ms.append((e0, e1))
@@ -415,13 +418,13 @@ def main():
     # work of this rank's launch, counted by the counting kernel outside the timed region: the
     # work the renderer executes (roofline) and the reference algorithm's work
     n_loc = len(tiles)
-    pix_local = sum(min(TILE, W - int(x)) * min(TILE, H - int(y)) for x, y in tiles)
+    pix_local = sum(min(tile, W - int(x)) * min(tile, H - int(y)) for x, y in tiles)
 
     def count_pass(flags):
         ctr = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
         tmp = torch.zeros(max(n_loc, 1) * tpix * 4, dtype=torch.int32, device=dev)
         cparams = rrt.render_params(W, H, ns_aa=wl["spp"], max_ray_depth=depth, flags=rrt.RRT_RENDER_COUNTERS | flags)
-        r.render_tiles_device(cparams, tiles, TILE, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
+        r.render_tiles_device(cparams, tiles, tile, tmp.data_ptr(), tmp.data_ptr() + n_loc * tpix * 3 * 4,
                               d_counters=ctr.data_ptr(), stream=s_handle)
         torch.cuda.synchronize()
         c4 = ctr.view(-1, 4).to(torch.int64).sum(0).cpu().numpy()
@@ -477,8 +480,8 @@ def main():
             "data": ("generated torus-knot scene (rrt_scenes.py)" if wl["dae"].startswith("@") else
                      "reference scene asset") + " via the native COLLADA ingest" +
                     (", generated HDR sky envmap (rrt_scenes.py)" if env is not None else "") + ", keyed RNG seed 0",
-            "config": {"workload": wl["desc"], "frame": [W, H], "spp": wl["spp"], "tile": TILE,
-                       "partition": (f"block-cyclic {TILE}x{TILE} tiles over {world} GPUs, RCCL gather to rank 0"
+            "config": {"workload": wl["desc"], "frame": [W, H], "spp": wl["spp"], "tile": tile,
+                       "partition": (f"lattice deal of {tile}x{tile} tiles over {world} GPUs, RCCL gather to rank 0"
                                      if world > 1 else "whole frame on 1 GPU, no gather")},
             "verified": verified,
             "verify": verify_note,

@@ -1763,27 +1763,6 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
       }
     }
   }
-  // Kerr continuations.  The Kerr build has no pixel pass (the miss proofs are
-  // the Schwarzschild stepper's), so no heavy list; in launches of at most 60% of the frame (a
-  // rank's share) of three or more adaptive steps a pixel, its groups hand a pixel with two or more
-  // steps to go to a waiting heavy block of the Kerr build (256 draw-offset slots a round).  cfg5
-  // (1024 spp) split 8 ways ended each rank's launch on a few pixels of 32 steps near the hole.
-  if (batch && kerr && c->hole.r > 0.0 && kp.draws_hit % kp.draws_miss == 0 && !(p->flags & RRT_RENDER_NO_HEAVY)) {
-    const uint64_t frame_px = (uint64_t)p->frame_w * p->frame_h;
-    const bool part = (uint64_t)kp.n_pixels * 5u <= frame_px * 3u;
-    const char* ce = std::getenv("RRT_AB_CONT");
-    if (p->ns_aa >= 3u * p->samples_per_batch && (ce ? ce[0] == '1' : part)) {
-      if (c->heavy_list_cap < 1) {  // the kernels read the (empty) list's counters
-        hipFree(c->d_heavy_list); c->d_heavy_list = nullptr;
-        HIPCHK(c, hipMalloc(&c->d_heavy_list, sizeof(uint32_t) * 4096u));
-        c->heavy_list_cap = 4096u;
-      }
-      kp.heavy_list = c->d_heavy_list;
-      kp.heavy_count = c->d_counter + RRT_QUEUE_STRIDE * (RRT_MAX_QUEUES + 1);
-      kp.heavy_cap = 0;
-      if (!setup_cont(part)) return RRT_E_HIP;
-    }
-  }
   // The bounce (depth >= 2) per-pixel-loop kernel behind the pixel miss proof pass: a proven
   // pixel's samples all miss at any depth (est_radiance returns the black miss, 2 draws each), so
   // the pass writes it and the kernel claims only the listed pixels, 64 per wave, in a
@@ -1881,8 +1860,7 @@ static int launch(rrt_ctx* c, const rrt_render_params* p, const uint32_t* tiles,
   // waves per heavy pixel: 2 (a 64-sample pixel's two steps in one round), 4 with continuations
   // (256 slots a round: the rest of a 256-sample pixel); A/B: variant bits 20..21 = 1 / 2 / 3:
   // 1 (2 for the point-light build) / 4 / 2
-  const int heavy_nw = lean == 3 ? 4 /* the Kerr build's only heavy kernel */
-                       : nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : nwv == 2 ? 4 : 2;
+  const int heavy_nw = nwv == 0 ? (kp.cont ? 4 : 2) : nwv == 1 ? (lean == 2 ? 2 : 1) : nwv == 2 ? 4 : 2;
   // heavy waves: hgv x the CU count (default 2), in blocks of heavy_nw waves
   const uint32_t heavy_waves = std::min<uint32_t>((uint32_t)c->n_cu * (hgv ? hgv : 2u), (uint32_t)c->n_cu * 4u);
   const uint32_t heavy_grid = std::max<uint32_t>(1u, heavy_waves / (uint32_t)heavy_nw);

@@ -508,20 +508,15 @@ __device__ __noinline__ void heavy_pixel_block(const KParams& kp, rrt::ShadeLdsN
     const v3 w = (smul(vx, ld3(cam.c2w0)) + smul(vy, ld3(cam.c2w1))) + smul(-1.0, ld3(cam.c2w2));
     const v3 wd = unit(w);
     Isect is;
-    constexpr bool KERR = LEAN == V_KERR;
-    const bool hit = t < lim && !camera_proven_miss<false, KERR>(kp, ld3(cam.pos), wd, cn) &&
-                     query_nx<false, false, KERR, 0, is_lean(LEAN)>(kp, ld3(cam.pos), wd, &is, cn);
+    const bool hit = t < lim && !camera_proven_miss<false, false>(kp, ld3(cam.pos), wd, cn) &&
+                     query_nx<false, false, false>(kp, ld3(cam.pos), wd, &is, cn);
     spec s = S(0, 0, 0);
-    if (hit) {  // est_radiance_global_illumination (part1_code.cpp:103-123), as the batch kernel shades
+    if (hit) {
       park_hit(sh, t, is);
       g.ctr = sl * Dm + Dm;
       const spec e = emission(kp.bsdfs[lget(sh.bsdf, t)]);
       if (kp.max_ray_depth == 0) s = e;
-      else if constexpr (is_lean(LEAN)) s = e + direct_importance_parked<false, LEAN, W>(kp, g, sh, t, cn);
-      else if (kp.direct_hemisphere) s = e + direct_hemisphere_parked<false, LEAN>(kp, g, sh, t, cn);
       else s = e + direct_importance_parked<false, LEAN, W>(kp, g, sh, t, cn);
-    } else if (!is_lean(LEAN) && t < lim && kp.env.w) {
-      s = env_dir(kp.env, wd);  // miss: envLight->sample_dir of the unbent camera ray
     }
     const uint64_t hb = __ballot(hit);
     if ((t & 63u) == 0) hs.hits[t >> 6] = hb;
@@ -634,8 +629,6 @@ hipError_t rrt_launch_heavy(const KParams* d_kp, int lean, int waves, int nw, ui
     }
   } else if (lean == 2) {
     if (nw == 4) RRT_LAUNCH_H(2, 4, 4); else RRT_LAUNCH_H(2, 4, 2);
-  } else if (lean == rrt::V_KERR) {  // continuations only (no pixel pass), the Kerr build's register budget
-    RRT_LAUNCH_H(rrt::V_KERR, 3, 4);
   } else {
     return hipErrorInvalidValue;
   }

@@ -343,7 +343,7 @@ def partition_tiles(frame_w, frame_h, tile_size, rank, world):
 
 
 def region_tiles(x0, y0, w, h, tile_size, rank, world):
-    """rrt_region_tiles: rank's tiles of the region's block-cyclic deal (rrt_group_render's split)."""
+    """rrt_region_tiles: rank's tiles of the region's lattice deal (rrt_group_render's split)."""
     n = lib().rrt_region_tiles(x0, y0, w, h, tile_size, rank, world, None, 0)
     if n < 0:
         raise RRTError(n, "bad partition arguments")

@@ -1,5 +1,5 @@
-"""Multi-GPU frame assembly: one process per GPU, block-cyclic 32x32 tiles, one
-gather to rank 0.
+"""Multi-GPU frame assembly: one process per GPU, 32x32 tiles dealt as a lattice
+(rrt_partition_tiles: tile (tx, ty) to rank (tx + S ty) % world), one gather to rank 0.
 
 Every rank renders the tiles rrt_partition_tiles gives it into one packed buffer (int32 words:
 [n_max * T^2 * 3] f32 RGB, then [n_max * T^2] i32 sample counts; tile t's pixel (i, j) at

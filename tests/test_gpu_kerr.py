@@ -120,30 +120,17 @@ def cfg5_region(c, sub):
     return None if sub is None else (c.x0 + sub[0], c.y0 + sub[1], sub[2], sub[3])
 
 
-# continuations of the Kerr build (a crop is a small part of the frame, so they
-# are on by default): off, and eager (every pixel that fails a check with 32 samples to go)
-CONT_ENV = {"nocont": {"RRT_AB_CONT": "0"}, "eager": {"RRT_AB_CONT": "1", "RRT_AB_CONT_MIN": "32"}}
-
-
-@pytest.mark.parametrize("variant", ["default", "onequeue", "noproof", "nocont", "eager"])
+@pytest.mark.parametrize("variant", ["default", "onequeue", "noproof"])
 @pytest.mark.parametrize("name,sub", CFG5)
-def test_kerr_cfg5_framing(gpu, name, sub, variant, monkeypatch):
+def test_kerr_cfg5_framing(gpu, name, sub, variant):
     """The benched cfg5 workload's own framing: GPU == restatement bit for bit (RGB, sample
-    counts, RNG draws), Kerr + environment light + adaptive 1024 spp; with the pixels that need
-    more steps resumed by the Kerr heavy blocks (continuations) and without."""
+    counts, RNG draws), Kerr + environment light + adaptive 1024 spp."""
     c = Case(name)
     reg = cfg5_region(c, sub)
-    for k, v in CONT_ENV.get(variant, {}).items():
-        monkeypatch.setenv(k, v)
     ref_rgb, ref_cnt, ref_draws, _ = oracle_render(c, 0.9, (0.0, 1.0, 0.0), region=reg)
-    rgb, cnt, draws, _ = gpu_render(gpu, c, 0.9, (0.0, 1.0, 0.0), flags=VARIANTS.get(variant, 0), region=reg)
+    rgb, cnt, draws, _ = gpu_render(gpu, c, 0.9, (0.0, 1.0, 0.0), flags=VARIANTS[variant], region=reg)
     m = parity_metrics(ref_rgb, rgb)
-    n_cont = gpu.stats().last_cont_pixels
-    print(variant, name, m, "samples", int(cnt.sum()), "mean", rgb.mean(axis=(0, 1)), "continuations", n_cont)
-    if variant == "nocont":
-        assert n_cont == 0
-    if variant == "eager" and int(cnt.max()) > 64:
-        assert n_cont > 0
+    print(variant, name, m, "samples", int(cnt.sum()), "mean", rgb.mean(axis=(0, 1)))
     assert c.exact and float(ref_rgb.max()) > 0
     assert np.array_equal(rgb.view(np.uint32), ref_rgb.view(np.uint32)), m
     assert np.array_equal(cnt, ref_cnt)

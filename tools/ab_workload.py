@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--workload", default="cfg5", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--world", type=int, default=1)
-    ap.add_argument("--tile", type=int, default=32, help="tile size of the split (bench.py: 32)")
+    ap.add_argument("--tile", type=int, default=0, help="tile size of the split (default: bench.py's for the workload)")
     ap.add_argument("--split", default="lib", help="lib (rrt_partition_tiles), latS: rank = (tx + S ty) %% world, "
                     "serS: serpentine index k, rank = (k + S ty) %% world")
     ap.add_argument("--rotate", action="store_true", help="round r renders the ranks from rank r %% world on "
@@ -38,7 +38,7 @@ def main():
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
-    W, H, ts = wl["w"], wl["h"], a.tile
+    W, H, ts = wl["w"], wl["h"], a.tile or wl.get("tile", bench.TILE)
     work = tempfile.mkdtemp(prefix="rrt_ab_")
     r = rrt.Renderer(0)
     scene, cam, _, _ = bench.load_workload_scene(wl, work)

@@ -155,6 +155,23 @@ for step in "$@"; do
     phase4r) # cfg4 ranks 6 and 3 of the 8-way (lattice) split on the profile build
            RRT_LIB=tools/librrt_prof.so run ph4_r6 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 --rank 6 8 &&
            RRT_LIB=tools/librrt_prof.so run ph4_r3 300 python3 tools/phase_profile.py --workload cfg4 --flags 0 --rank 3 8 ;;
+    ab3)   # claim order (back part first), tail-priority threshold, 16 / 8-px tiles: 8-way splits and whole frames
+           run ab3_c3 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 --rotate 0 0:0:RRT_AB_BACK_FIRST=1 0:0:RRT_AB_PRIO_TICKS=10000 0:0:RRT_AB_PRIO_TICKS=25000 &&
+           run ab3_c3t16 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 --rotate --tile 16 0 0:0:RRT_AB_BACK_FIRST=1 &&
+           run ab3_c4 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate 0 0:0:RRT_AB_PRIO_TICKS=10000 0:0:RRT_AB_PRIO_TICKS=25000 &&
+           run ab3_c4t16 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate --tile 16 0 &&
+           run ab3_c5t16 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate --tile 16 0:0:RRT_AB_CONT=0 &&
+           run ab3_c5t8 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate --tile 8 0:0:RRT_AB_CONT=0 &&
+           run ab3_w3 600 python3 tools/ab_workload.py --workload cfg3 --rounds 5 0 0:0:RRT_AB_PRIO_TICKS=25000 &&
+           run ab3_w3t16 600 python3 tools/ab_workload.py --workload cfg3 --rounds 5 --tile 16 0 &&
+           run ab3_w4 600 python3 tools/ab_workload.py --workload cfg4 --rounds 3 0 &&
+           run ab3_w4t16 600 python3 tools/ab_workload.py --workload cfg4 --rounds 3 --tile 16 0 &&
+           run ab3_w5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 &&
+           run ab3_w5t16 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 --tile 16 0 ;;
+    w8all) # 8-way projections of the BASELINE configs on this build (every rank's tiles on one GPU, rotated order)
+           run w8_cfg3 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 --rotate 0 &&
+           run w8_cfg4 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate 0 &&
+           run w8_cfg5 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
