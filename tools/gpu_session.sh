@@ -172,6 +172,12 @@ for step in "$@"; do
            run w8_cfg3 600 python3 tools/ab_workload.py --workload cfg3 --world 8 --rounds 3 --rotate 0 &&
            run w8_cfg4 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate 0 &&
            run w8_cfg5 600 python3 tools/ab_workload.py --workload cfg5 --world 8 --rounds 2 --rotate 0 ;;
+    abflags) # scheduler flag variants of the whole library (tools/build_variant.sh) against the in-tree build
+           bash tools/ab_libs.sh cfg3 3 base sink sinktrk && bash tools/ab_libs.sh cfg4 2 base sink sinktrk &&
+           bash tools/ab_libs.sh cfg5 1 base sink sinktrk && bash tools/ab_libs.sh m3 1 base sink sinktrk &&
+           bash tools/ab_libs.sh cfg2 2 base sink sinktrk ;;
+    final) # the round's final evidence: GPU suite, smoke, every bench line, kernel stats, PMC, 8-way projections
+           RTAG=${RTAG:-r06} bash tools/gpu_session.sh test smoke benchall w8all profall || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
