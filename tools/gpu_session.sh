@@ -178,6 +178,15 @@ for step in "$@"; do
            bash tools/ab_libs.sh cfg2 2 base sink sinktrk ;;
     final) # the round's final evidence: GPU suite, smoke, every bench line, kernel stats, PMC, 8-way projections
            RTAG=${RTAG:-r06} bash tools/gpu_session.sh test smoke benchall w8all profall || exit $? ;;
+    abwaves6) # waves/SIMD budgets of the batch kernels on the sink build (variant = waves), whole frames
+           run abw6_c3 600 python3 tools/ab_workload.py --workload cfg3 --rounds 4 0 3 5 &&
+           run abw6_c4 600 python3 tools/ab_workload.py --workload cfg4 --rounds 3 0 4 &&
+           run abw6_c2 600 python3 tools/ab_workload.py --workload cfg2 --rounds 3 0 3 5 &&
+           run abw6_c5 900 python3 tools/ab_workload.py --workload cfg5 --rounds 1 0 2 4 ;;
+    abflags2) # more build flags on top of the sink build: no loop unrolling, size-mode live-range splitting
+           bash tools/ab_libs.sh cfg3 3 base nounroll ssize && bash tools/ab_libs.sh cfg4 2 base nounroll ssize &&
+           bash tools/ab_libs.sh cfg2 2 base nounroll ssize && bash tools/ab_libs.sh cfg5 1 base nounroll ssize &&
+           bash tools/ab_libs.sh m3 1 base nounroll ssize ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
