@@ -117,6 +117,13 @@ def test_tile_deal_matches_frame_plan(world):
             assert np.array_equal(rrt.region_tiles(0, 0, W, H, 32, q, world), want)
         assert plan.n_max == max(len(plan.tiles(q)) for q in range(world))
         assert sorted(map(tuple, np.concatenate([plan.tiles(q) for q in range(world)]).tolist())) == sorted(order)
+    # bench.py's cfg5 split: 16-px tiles of the 4K frame, the same rule
+    W, H, T = 3840, 2160, 16
+    plan = rrt_frame.FramePlan(W, H, world, T)
+    got = np.concatenate([plan.tiles(q) for q in range(world)])
+    assert len(got) == (W // T) * (H // T) == len({tuple(t) for t in got.tolist()})
+    for q in range(world):
+        assert all((x // T + S * (y // T)) % world == q for x, y in plan.tiles(q).tolist())
     # a region (rrt_group_render): tiles from the region's origin, the same deal
     x0, y0, w, h = 70, 13, 200, 65
     rt = [rrt.region_tiles(x0, y0, w, h, 32, q, world) for q in range(world)]
