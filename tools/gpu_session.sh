@@ -187,6 +187,11 @@ for step in "$@"; do
            bash tools/ab_libs.sh cfg3 3 base nounroll ssize && bash tools/ab_libs.sh cfg4 2 base nounroll ssize &&
            bash tools/ab_libs.sh cfg2 2 base nounroll ssize && bash tools/ab_libs.sh cfg5 1 base nounroll ssize &&
            bash tools/ab_libs.sh m3 1 base nounroll ssize ;;
+    w24all) # 2- and 4-way projections of the BASELINE configs (every rank's tiles on one GPU, rotated order)
+           for n in 2 4; do
+             run w${n}_cfg3 600 python3 tools/ab_workload.py --workload cfg3 --world $n --rounds 3 --rotate 0 || exit $?
+             run w${n}_cfg4 600 python3 tools/ab_workload.py --workload cfg4 --world $n --rounds 3 --rotate 0 || exit $?
+             run w${n}_cfg5 900 python3 tools/ab_workload.py --workload cfg5 --world $n --rounds 1 --rotate 0 || exit $?; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
