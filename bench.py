@@ -11,8 +11,9 @@ generated 100k-triangle torus-knot scene (rrt_scenes.py; CBdragon.dae is missing
 3840x2160, 256 spp; --workload cfg5 runs configs[4]: the Kerr integrator (a/M 0.9)
 with the generated HDR sky environment map, CBbunny at 3840x2160, 1024 spp.
 
-One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's 32x32
-tiles are dealt over the ranks as a lattice (rrt_partition_tiles); every rank renders its tiles into a
+One step = one full frame.  With N GPUs (one process per GPU, torchrun) the frame's tiles
+(32x32; 16x16 for cfg5) are dealt over the ranks as a lattice (rrt_partition_tiles: tile (tx, ty)
+to rank (tx + S ty) % N); every rank renders its tiles into a
 packed buffer and rank 0 gathers them over RCCL and unpacks them into the frame (the only
 exchange step).  Total work is fixed, so scaling is "strong".
 
