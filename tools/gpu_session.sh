@@ -192,6 +192,9 @@ for step in "$@"; do
              run w${n}_cfg3 600 python3 tools/ab_workload.py --workload cfg3 --world $n --rounds 3 --rotate 0 || exit $?
              run w${n}_cfg4 600 python3 tools/ab_workload.py --workload cfg4 --world $n --rounds 3 --rotate 0 || exit $?
              run w${n}_cfg5 900 python3 tools/ab_workload.py --workload cfg5 --world $n --rounds 1 --rotate 0 || exit $?; done ;;
+    abknobs4) # the continuation / heavy-kernel run-time knobs on the lattice deal (cfg4 8-way): room, samples left,
+           # heavy waves 3x CU (variant bits 28..31), heavy kernel at 5 waves/SIMD (bits 24..27)
+           run abknobs4 600 python3 tools/ab_workload.py --workload cfg4 --world 8 --rounds 3 --rotate 0 0:0:RRT_AB_CONT_ROOM=64 0:0:RRT_AB_CONT_MIN=32 805306368 83886080 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
